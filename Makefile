@@ -1,0 +1,54 @@
+# Top-level build: the product library (HIP for gfx950) and the test oracle.
+#
+#   make            -> voxelraytrace20190722_amd/libvrt.so + oracle/liboracle.so
+#                      (+ oracle/_ref/libvrtref.so when /root/reference exists)
+#
+# Float contract: -ffp-contract=off (no FMA contraction, host or device), no
+# fast-math; hipcc keeps correctly rounded f32 division and sqrt by default.
+
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := voxelraytrace20190722_amd
+SRC := $(PKG)/csrc
+BLD := build/obj
+FP := -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt
+HIPFLAGS := -x hip --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 $(FP) -Iinclude -I$(SRC) \
+            -Wall -Wno-unused-function -fvisibility=hidden
+CXXFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Wall -fvisibility=hidden
+
+OBJS := $(BLD)/vrt_kernels.o $(BLD)/vrt_host.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o
+HDRS := include/vrt.h $(SRC)/vrt_math.h $(SRC)/vrt_internal.h
+
+all: $(PKG)/libvrt.so oracle
+
+$(BLD):
+	mkdir -p $(BLD)
+
+$(BLD)/vrt_kernels.o: $(SRC)/vrt_kernels.hip $(HDRS) | $(BLD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BLD)/vrt_host.o: $(SRC)/vrt_host.cpp $(HDRS) | $(BLD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BLD)/vrt_hdr.o: $(SRC)/vrt_hdr.cpp include/vrt.h | $(BLD)
+	g++ $(CXXFLAGS) -c $< -o $@
+
+$(BLD)/vrt_proxy.o: $(SRC)/vrt_proxy.cpp include/vrt.h | $(BLD)
+	g++ $(CXXFLAGS) -c $< -o $@
+
+$(PKG)/libvrt.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+# ISA listing + register/occupancy report of the kernels (for DESIGN.md)
+isa: | $(BLD)
+	$(HIPCC) $(HIPFLAGS) --offload-device-only -S $(SRC)/vrt_kernels.hip -o $(BLD)/vrt_kernels.s \
+	  -Rpass-analysis=kernel-resource-usage 2> $(BLD)/resource_usage.txt || true
+
+clean:
+	rm -rf build $(PKG)/libvrt.so
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle isa clean

@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s of the primary-ray hot path (camera ray generation +
+voxel-octree ray march + Moller-Trumbore + primary shading + Film
+accumulation) at 1920x1080 on the sponza-proxy, max_depth 8 ("256^3",
+BASELINE.json configs[1]), over the 16-pose camera sweep.
+
+One process per GPU.  A step = one 1920x1080 frame (4 samples / pixel) at
+sweep pose (step % 16): each rank renders its share of the 8x8-pixel tiles
+(tile t -> rank t % N), then one RCCL gather of the per-rank tile buffers to
+rank 0, which re-assembles the image (scaling "strong": the frame is fixed).
+Inputs (octree, triangles, textures) are resident in HBM before timing.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line on stdout; diagnostics go to stderr.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch  # noqa: E402  (import torch before libvrt: one HIP runtime)
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import voxelraytrace20190722_amd as vrt  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=32)
+    p.add_argument("--warmup", type=int, default=4)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--depth", type=int, default=8, help="max_depth; '256^3' = log2(256) = 8")
+    p.add_argument("--detail", type=float, default=1.0, help="proxy tessellation (1.0 ~ 262k tris)")
+    p.add_argument("--poses", type=int, default=16)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-counters", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={a.gpus}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    # ---- scene: built on the host, uploaded once (excluded from timing)
+    t0 = time.time()
+    sd = vrt.SceneData.proxy(a.detail, 1)
+    tree = vrt.VoxelOctree(sd, a.depth, device=local)
+    info = tree.info
+    log(f"[rank {rank}] scene: {sd.ntri} tris, depth {a.depth}: {info.nodes} nodes, "
+        f"{info.nonempty_leaves} non-empty leaves, {info.tri_refs} refs, "
+        f"{info.device_bytes / 2**20:.1f} MiB on device; build {info.build_ms:.0f} ms, "
+        f"upload {info.upload_ms:.0f} ms ({time.time() - t0:.1f} s total)")
+    mn, mx = tree.root_box
+    cams = []
+    for i in range(a.poses):
+        fov, eye, spot, up = vrt.sweep_pose(mn, mx, i, a.poses)
+        cams.append(vrt.Camera(fov, eye, spot, up))
+    film = vrt.Film(1.0, 1.0, a.width, a.height)
+    W8, H8 = 8 * (a.width // 8), 8 * (a.height // 8)
+    rays_per_frame = W8 * H8 * 4
+
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    tpr = vrt.tiles_per_rank(film, world)
+    img = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev)
+    if world > 1:
+        tiles = torch.zeros(tpr * 192, dtype=torch.float32, device=dev)
+        gl = [torch.zeros_like(tiles) for _ in range(world)] if rank == 0 else None
+        gathered = torch.zeros((world, tpr * 192), dtype=torch.float32, device=dev) if rank == 0 else None
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(a.steps)]
+
+    def step(k, timed):
+        cam = cams[k % a.poses]
+        if timed:
+            ev[k][0].record(stream)
+        if world == 1:
+            tree.render_tiles_device(cam, film, 0, 1, 1, img.data_ptr(), sp)
+            if timed:
+                ev[k][1].record(stream)
+            return
+        tree.render_tiles_device(cam, film, rank, world, 0, tiles.data_ptr(), sp)
+        if timed:
+            ev[k][1].record(stream)
+        dist.gather(tiles, gl, dst=0)
+        if rank == 0:
+            torch.stack(gl, out=gathered)
+            vrt.unpack_tiles_device(film, world, gathered.data_ptr(), img.data_ptr(), sp)
+
+    for k in range(a.warmup):
+        step(k, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(a.steps):
+        step(k, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kms = np.array([s.elapsed_time(e) for s, e in ev])  # render kernel, ms
+
+    # ---- algorithmic bytes from the instrumented kernel's
+    # reference-equivalent counters, per pose actually rendered
+    roof = None
+    if not a.no_counters:
+        poses_used = sorted({k % a.poses for k in range(a.steps)})
+        b_rank = []
+        cnt_tot = np.zeros(4)
+        for pi in poses_used:
+            _, so = tree.render(cams[pi], film, counters=True)
+            c = so["counters"].reshape(a.height, a.width, 4, 4)
+            # this rank's tiles only
+            ty, tx = np.divmod(np.arange((a.width // 8) * (a.height // 8)), a.width // 8)
+            mine = (np.arange(len(tx)) % world) == rank
+            m = np.zeros((H8 // 8, W8 // 8), bool)
+            m[ty[mine], tx[mine]] = True
+            mask = np.repeat(np.repeat(m, 8, 0), 8, 1)
+            cc = c[:H8, :W8][mask].reshape(-1, 4).astype(np.float64)
+            s = cc.sum(0)
+            cnt_tot += s
+            npx = mask.sum()
+            b_rank.append(28 * s[0] + 8 * s[1] + 40 * s[2] + 68 * s[3] + 12 * npx)
+        pose_b = dict(zip(poses_used, b_rank))
+        bytes_per_launch = np.mean([pose_b[k % a.poses] for k in range(a.steps)])
+        achieved = bytes_per_launch / (kms.mean() * 1e-3) / 1e9
+        traffic = None
+        try:
+            tj = json.load(open(a.traffic_json))
+            key = f"{a.width}x{a.height}_d{a.depth}_n{world}"
+            traffic = tj.get(key)
+        except Exception:
+            pass
+        nr = cnt_tot[3] and (cnt_tot / (len(poses_used) * rays_per_frame / world))
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                "algorithmic_bytes_per_launch": round(float(bytes_per_launch)),
+                "per_ray": {"A": round(float(nr[0]), 2), "L": round(float(nr[1]), 2),
+                            "T": round(float(nr[2]), 2), "H": round(float(nr[3]), 3)}}
+
+    # ---- CPU baseline: the oracle (C restatement of the reference path,
+    # render_mt-style 8x8 tiles over pthreads) on a bounded row sample
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as po
+        osc = po.Scene(sd, a.depth)
+        fov, eye, spot, up = vrt.sweep_pose(mn, mx, 0, a.poses)
+        oc = po.camera(fov, eye, spot, up)
+        nth = max(1, min(a.cpu_threads, os.cpu_count() or 1))
+        stride = 64
+        sec, _ = osc.render_rows(oc, 1.0, 1.0, a.width, a.height, stride, 0, nth)
+        rows = len(range(0, H8, stride))
+        rate = rows * W8 * 4 / max(sec, 1e-6)
+        want_rows = max(1, int(rate * a.cpu_seconds / (W8 * 4)))
+        stride = max(1, H8 // want_rows)
+        sec, _ = osc.render_rows(oc, 1.0, 1.0, a.width, a.height, stride, 0, nth)
+        rows = len(range(0, H8, stride))
+        cpu_rays = rows * W8 * 4
+        cpu = {"value": round(cpu_rays / sec / 1e6, 4), "unit": "Mrays/s", "cores": nth, "kind": "port",
+               "sample": f"every {stride}th row ({rows} rows x {W8} px x 4 spp = {cpu_rays} rays) of the "
+                         f"{a.width}x{a.height} frame at sweep pose 0, {sec:.1f} s, oracle/vrt_oracle.c "
+                         f"over {nth} threads"}
+        osc.close()
+
+    if rank == 0:
+        total_rays = rays_per_frame * a.steps
+        value = total_rays / elapsed / 1e6
+        out = {
+            "metric": "Mrays/s at 1920x1080 Sponza 256^3 octree (primary rays, 4 spp)",
+            "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32+f64",
+            "data": "synthetic: deterministic sponza-proxy atrium (sponza.obj absent), 16-pose camera sweep",
+            "config": {"workload": f"primary render {a.width}x{a.height} x4 spp, sponza-proxy "
+                                   f"({sd.ntri} tris), max_depth {a.depth} (\"256^3\")",
+                       "width": a.width, "height": a.height, "max_depth": a.depth,
+                       "rays_per_frame": rays_per_frame, "tris": sd.ntri, "poses": a.poses,
+                       "parallelism": f"screen tiles x{world}" + (" + rccl gather" if world > 1 else "")},
+            "kernel_ms_mean": round(float(kms.mean()), 4),
+            "kernel_mrays_per_s": round(rays_per_frame / world / (kms.mean() * 1e-3) / 1e6, 2),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,231 @@
+/*
+ * vrt.h -- C ABI of the MI355X-native voxel-octree ray-march hot path
+ * (drop-in for jqly/VoxelRayTrace20190722's per-pixel primary-ray loop).
+ *
+ * libvrt.so (voxelraytrace20190722_amd/libvrt.so) exports exactly the symbols
+ * below.  Conventions: plain pointers and sizes, caller-owned outputs, opaque
+ * handles, int status codes (VRT_OK = 0, negative = error; the legacy
+ * symbols keep the reference's 1/0 returns), no exceptions or exit() across
+ * the ABI.  Reference citations: VRT/x = VoxelRayTrace20190722/x.
+ */
+#ifndef VRT_H
+#define VRT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+#pragma GCC visibility push(default)
+
+#define VRT_OK 0
+#define VRT_E_INVALID (-1)  /* bad argument (NULL, size, depth, id range) */
+#define VRT_E_NOMEM (-2)    /* host allocation failed */
+#define VRT_E_DEVICE (-3)   /* HIP runtime error (see vrt_last_error) */
+#define VRT_E_NODEVICE (-4) /* no usable gfx950 device */
+#define VRT_E_IO (-5)       /* file could not be written */
+
+#define VRT_MAX_DEPTH 11    /* voxel ids pack 10 bits per axis */
+
+typedef struct vrt_scene vrt_scene;
+
+/* Triangle soup in obj2voxel's output order (VRT/voxel_octree.cc:305-371);
+ * triangle i is gi::Triangle{p0,p1,p2,n0,n1,n2,t0,t1,t2,mtl}
+ * (VRT/voxel_octree.h:94-113).  Normals are normalised by the build exactly
+ * like Triangle::Triangle (VRT/voxel_octree.cc:426). */
+typedef struct {
+        int32_t ntri;
+        const float *pos;      /* ntri*9 */
+        const float *nrm;      /* ntri*9 */
+        const float *uv;       /* ntri*6, NULL = all zero (texcoord_index -1) */
+        const int32_t *mat;    /* ntri,   NULL = all material 0 */
+        int32_t nmat;          /* >= 1 */
+        const int32_t *mat_tex;/* nmat texture ids, -1 = untextured (Kd) */
+        const float *mat_kd;   /* nmat*3 tinyobj material_t::diffuse */
+        int32_t ntex;
+        const int32_t *tex_dims;  /* ntex*3 {width, height, channels 1..4} */
+        const int64_t *tex_off;   /* ntex byte offsets into tex_data */
+        const uint8_t *tex_data;  /* stbi_load(...,0) bytes, row 0 = top */
+        int64_t tex_bytes;
+} vrt_scene_desc;
+
+/* jql::Ray after construction (VRT/graphics_math.h:1150-1167): d is already
+ * normalised; tmin/tmax bound AABB3D::isect (VRT/graphics_math.h:1312). */
+typedef struct {
+        float o[3];
+        float d[3];
+        float tmin, tmax;
+} vrt_ray;
+
+/* Camera (VRT/camera.h:70-84): C = affine_transform(Mat3{s,up_,-fwd}, eye),
+ * column-major.  `origin` = point_transform(C,{}) is cached; the film plane
+ * z = -(film.h / (2*tanf(fov/2))) is evaluated on the host per film. */
+typedef struct {
+        float C[16];
+        float fov, near_, far_;
+        float origin[3];
+} vrt_camera;
+
+/* Film (VRT/camera.h:24-39): physical w,h and pixel counts nx,ny. */
+typedef struct {
+        float w, h;
+        int32_t nx, ny;
+} vrt_film;
+
+/* One gi::ray_march result (VRT/voxel_octree.h:87-89). */
+typedef struct {
+        int32_t hit;      /* 1 = ray_march returned true */
+        int32_t tri;      /* index of *voxel_ptr in the input soup, -1 */
+        uint32_t voxel;   /* *leaf_ptr's integer coords at max depth:
+                             ix | iy<<10 | iz<<20, 0xFFFFFFFF on a miss */
+        float hit_p[3];   /* ISect::hit */
+        float normal[3];  /* ISect::normal */
+} vrt_hit;
+
+typedef struct {
+        int64_t nodes, internal, leaves, nonempty_leaves, tri_refs;
+        int32_t max_depth, device;
+        float root_min[3], root_max[3];
+        int64_t device_bytes;
+        double build_ms, upload_ms;
+} vrt_scene_info_t;
+
+/* Optional per-sample outputs of vrt_render (host arrays, index
+ * ((py*nx+px)*4 + s), s = gen_rays4 sample order).  Any pointer may be NULL.
+ * counters = {A aabb tests, L leaves entered, T triangle tests, H hit} as
+ * the reference's ray_march performs them; requesting them
+ * selects the instrumented kernel variant. */
+typedef struct {
+        int32_t *hit;
+        int32_t *tri;
+        uint32_t *voxel;
+        float *rgb;       /* 3 per sample: get_diffuse / sky colour */
+        uint32_t *counters;
+} vrt_samples;
+
+/* Aggregate counters of one instrumented render (sums over all samples). */
+typedef struct {
+        uint64_t rays, aabb_tests, leaves, tri_tests, hits;
+        double kernel_ms;
+} vrt_stats;
+
+/* ---- device / scene ------------------------------------------------- */
+int vrt_device_count(int *n);
+/* gi::ray_march_init (VRT/voxel_octree.cc:67-75) on the host, then upload
+ * of the flattened octree + triangles + textures to `device`.  device < 0
+ * builds a host-only scene (info / leaves only; device calls then return
+ * VRT_E_NODEVICE). */
+int vrt_scene_create(const vrt_scene_desc *desc, int max_depth, int device,
+                     vrt_scene **out);
+void vrt_scene_destroy(vrt_scene *s);
+int vrt_scene_info(const vrt_scene *s, vrt_scene_info_t *info);
+/* Non-empty leaves sorted by voxel id; tris = concatenated leaf lists in
+ * insertion (input) order.  Sizes from vrt_scene_info. */
+int vrt_scene_leaves(const vrt_scene *s, uint32_t *voxel, uint32_t *count,
+                     int32_t *tris);
+
+/* ---- camera (host, VRT/camera.cc) ------------------------------------ */
+int vrt_camera_init(float fov, const float eye[3], const float spot[3],
+                    const float up[3], float near_, float far_,
+                    vrt_camera *out);
+int vrt_gen_rays4(const vrt_camera *cam, const vrt_film *film, int px, int py,
+                  vrt_ray out[4]);
+int vrt_gen_rays1(const vrt_camera *cam, const vrt_film *film, int px, int py,
+                  vrt_ray out[1]);
+/* jql::Ray::Ray(o, d, tmin, tmax): normalises d. */
+int vrt_make_ray(const float o[3], const float d[3], float tmin, float tmax,
+                 vrt_ray *out);
+/* AABB3D::isect(ray, nullptr) on the host (box = min xyz, max xyz). */
+int vrt_aabb_isect(const float box[6], const vrt_ray *ray);
+
+/* ---- the hot path ------------------------------------------------------ */
+/* Primary render = the per-pixel loop of VRT/main.cc:118-123 with the
+ * primary shading contract (hit: Triangle::get_diffuse(isect, ray, (1,1,1));
+ * miss: sky lerp, VRT/main.cc:18-20), 4 gen_rays4 samples accumulated with
+ * Film::add(c * .25f).  Pixels outside render_mt's 8x8 tile grid
+ * (px >= 8*(nx/8) or py >= 8*(ny/8), VRT/camera.h:45-61) stay 0.
+ * Film index is y*nx+x (the reference's y*ny+x, VRT/camera.cc:19, agrees for
+ * square films).  rgb: host nx*ny*3 floats.  samples / stats may be NULL. */
+int vrt_render(vrt_scene *s, const vrt_camera *cam, const vrt_film *film,
+               float *rgb, const vrt_samples *samples, vrt_stats *stats);
+
+/* Device-resident variant (inputs/outputs in HBM, enqueued on `stream`, a
+ * hipStream_t or NULL for the null stream; no host synchronisation).
+ * Screen = 8x8-pixel tiles, row-major, t = 0..ntiles-1; this call renders
+ * tiles t = rank + k*nranks (k = 0..) into d_out packed tile-major:
+ * d_out[(k*64 + (y%8)*8 + x%8)*3 + c], sized vrt_tiles_per_rank()*192
+ * floats.  rank=0, nranks=1 with image_layout=1 writes the nx*ny*3 image
+ * directly instead. */
+int vrt_tiles_per_rank(const vrt_film *film, int nranks);
+int vrt_render_tiles_device(vrt_scene *s, const vrt_camera *cam,
+                            const vrt_film *film, int rank, int nranks,
+                            int image_layout, float *d_out, void *stream);
+/* Rank 0 after the gather: d_gathered = nranks * tiles_per_rank * 192 floats
+ * (rank-major) -> d_image nx*ny*3 (pixels outside the tile grid zeroed). */
+int vrt_unpack_tiles_device(const vrt_film *film, int nranks,
+                            const float *d_gathered, float *d_image,
+                            void *stream);
+/* Device time of the last render kernel enqueued by this thread on `s`
+ * (HIP events around the launch, on its stream). */
+int vrt_last_kernel_ms(vrt_scene *s, float *ms);
+
+/* Batched gi::ray_march (VRT/voxel_octree.cc:131-188) on host arrays. */
+int vrt_ray_march_batch(vrt_scene *s, const vrt_ray *rays, int64_t n,
+                        vrt_hit *hits);
+/* Device-resident variant (d_rays / d_hits in HBM). */
+int vrt_ray_march_batch_device(vrt_scene *s, const vrt_ray *d_rays, int64_t n,
+                               vrt_hit *d_hits, void *stream);
+
+/* Device copies of the fp64 Moller-Trumbore and fp32 SAT leaves (the exact
+ * code the kernels inline), run on n host-array cases for parity tests.
+ * mt_in: n*15 doubles {orig,dir,v0,v1,v2}; mt_out: n*4 doubles
+ * {ret, t, u, v} (t,u,v = 0 unless ret == 1).  sat_in: n*15 floats
+ * {center, half, tri[9]}; sat_out: n ints. */
+int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
+                        const float *sat_in, int32_t *sat_out, int64_t n);
+
+/* ---- output (VRT/stb_image_write.h:178,723-757) ------------------------- */
+/* Byte-identical to stbi_write_hdr: returns 1 on success, 0 on failure. */
+int vrt_write_hdr(const char *filename, int w, int h, int comp,
+                  const float *data);
+/* Same bytes into memory: returns the byte count, or -(needed) if cap is
+ * too small, or 0 on invalid input. */
+int64_t vrt_write_hdr_mem(int w, int h, int comp, const float *data,
+                          uint8_t *out, int64_t cap);
+
+/* ---- legacy reference symbols (identical signatures and results) ------- */
+/* VRT/raytri.h:5-7 */
+int intersect_triangle3(double orig[3], double dir[3], double vert0[3],
+                        double vert1[3], double vert2[3], double *t,
+                        double *u, double *v);
+/* VRT/tribox2.h:6 */
+int triBoxOverlap(float boxcenter[3], float boxhalfsize[3],
+                  float triverts[3][3]);
+
+/* ---- synthetic inputs ----------------------------------------------------
+ * Deterministic "sponza-proxy" atrium (no Sponza asset ships): floor, walls,
+ * two storeys of colonnades and arches, curtains, details; every material
+ * textured with procedural 8-bit textures.  `detail` scales tessellation
+ * (1.0 ~ 262k triangles).  Two-call protocol: call with NULL arrays to get
+ * counts in *ntri / *nmat / *ntex / *tex_bytes, then with arrays sized to
+ * them.  Bounds match the scaled Sponza frame the reference cameras use
+ * (VRT/main.cc:76-78,112-115). */
+int vrt_proxy_scene(double detail, uint32_t seed, int32_t *ntri, float *pos,
+                    float *nrm, float *uv, int32_t *mat, int32_t *nmat,
+                    int32_t *mat_tex, float *mat_kd, int32_t *ntex,
+                    int32_t *tex_dims, int64_t *tex_off, uint8_t *tex_data,
+                    int64_t *tex_bytes);
+/* Camera-sweep pose i of n: ellipse at 0.4 * AABB height around the AABB
+ * centre, looking at the centre, fov 90 degrees. */
+int vrt_sweep_pose(const float root_min[3], const float root_max[3], int i,
+                   int n, float eye[3], float spot[3], float up[3],
+                   float *fov);
+
+const char *vrt_status_string(int status);
+const char *vrt_last_error(void);
+
+#pragma GCC visibility pop
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,38 @@
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device")
+
+
+def _ensure_built():
+    need = [os.path.join(ROOT, "voxelraytrace20190722_amd", "libvrt.so"),
+            os.path.join(ROOT, "oracle", "liboracle.so")]
+    if all(os.path.exists(p) for p in need):
+        return
+    if shutil.which("make") is None:
+        raise RuntimeError("libraries missing and `make` unavailable")
+    subprocess.run(["make", "-j8"], cwd=ROOT, check=True)
+
+
+_ensure_built()
+
+
+def golden(name):
+    import numpy as np
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+@pytest.fixture(scope="session")
+def gold():
+    return golden

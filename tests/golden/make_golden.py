@@ -1,0 +1,169 @@
+"""Regenerate the committed golden fixtures (run in the dev container, where
+/root/reference exists):
+
+    python tests/golden/make_golden.py
+
+* kat_raytri.npz / kat_tribox.npz / hdr_ref.npz -- outputs of the
+  REFERENCE's own raytri.cc, tribox2.cc and stb_image_write.h, compiled
+  unmodified into oracle/_ref/libvrtref.so (oracle/Makefile).
+* scene_*.npz -- small scenes (inputs) with per-sample outputs of the oracle
+  restatement (oracle/vrt_oracle.c): hit, triangle id, voxel id, per-sample
+  RGB, reference-equivalent counters and the accumulated image.  The oracle's
+  floating-point leaves are pinned by the KATs above; see DESIGN.md.
+Only inputs and outputs are stored -- no reference source.
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import pyoracle as po  # noqa: E402
+
+import voxelraytrace20190722_amd as vrt  # noqa: E402
+
+
+def kat_raytri(n=6000, seed=7):
+    rng = np.random.default_rng(seed)
+    cases = []
+    # float-widened inputs, as Triangle::isect passes them
+    a = rng.standard_normal((n // 3, 15)).astype(np.float32).astype(np.float64)
+    cases.append(a)
+    # small-integer grids: edge / vertex / coplanar / parallel hits
+    b = (rng.integers(-3, 4, (n // 3, 15)) * 0.5).astype(np.float64)
+    cases.append(b)
+    # near-degenerate determinants around +-1e-6 and rays along axes
+    c = rng.standard_normal((n - 2 * (n // 3), 15)).astype(np.float32).astype(np.float64)
+    c[:, 3:6] = 0.0
+    ax = rng.integers(0, 3, len(c))
+    c[np.arange(len(c)), 3 + ax] = rng.choice([-1.0, 1.0], len(c))
+    scale = 10.0 ** rng.uniform(-4.5, -2.0, len(c))
+    c[:, 9:15] = c[:, 6:9].repeat(2, 0).reshape(len(c), 6) + (c[:, 9:15] * scale[:, None])
+    cases.append(c)
+    # rays aimed at a point of the triangle (hits, incl. near-edge / vertex
+    # barycentrics and hits behind the origin)
+    m = n // 2
+    tri = rng.standard_normal((m, 9)).astype(np.float32)
+    w = rng.dirichlet([1, 1, 1], m)
+    w[: m // 4] = np.round(w[: m // 4] * 8) / 8  # on edges / vertices
+    tgt = (w[:, :1] * tri[:, 0:3] + w[:, 1:2] * tri[:, 3:6] + w[:, 2:3] * tri[:, 6:9])
+    org = rng.standard_normal((m, 3)) * 3
+    d = tgt - org
+    d[: m // 8] *= -1  # target behind the origin: a hit with t < 0
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    cases.append(np.concatenate([org, d, tri], 1).astype(np.float32).astype(np.float64))
+    q = np.ascontiguousarray(np.concatenate(cases))
+    out = np.zeros((len(q), 4))
+    for i in range(len(q)):
+        r, t, u, v = po.ref_intersect_triangle3(q[i])
+        out[i] = (r, t, u, v) if r == 1 else (r, 0, 0, 0)
+    return q, out
+
+
+def kat_tribox(n=8000, seed=11):
+    rng = np.random.default_rng(seed)
+    a = rng.standard_normal((n // 2, 15)).astype(np.float32)
+    b = (rng.integers(-4, 5, (n - n // 2, 15)) * 0.25).astype(np.float32)
+    q = np.ascontiguousarray(np.concatenate([a, b]))
+    q[:, 3:6] = np.abs(q[:, 3:6])
+    out = np.array([po.ref_tri_box_overlap(q[i]) for i in range(len(q))], np.int32)
+    return q, out
+
+
+def hdr_cases(seed=3):
+    rng = np.random.default_rng(seed)
+    imgs = []
+    for (h, w, c) in [(5, 7, 3), (9, 40, 3), (16, 300, 3), (4, 130, 1), (6, 64, 4), (3, 9, 2)]:
+        x = (rng.random((h, w, c)) * 4).astype(np.float32)
+        x[:, : w // 3] = 0.25  # long runs
+        x[0, :] = 0.0
+        x[1, ::3] = 1e-33      # below the rgbe threshold
+        imgs.append(x)
+    return imgs
+
+
+def downsample_textures(sd, step):
+    dims, offs, data = [], [], []
+    o = 0
+    for t in range(len(sd.tex_off)):
+        w, h, c = sd.tex_dims[t]
+        img = sd.tex_data[sd.tex_off[t]: sd.tex_off[t] + w * h * c].reshape(h, w, c)[::step, ::step]
+        img = np.ascontiguousarray(img)
+        dims.append([img.shape[1], img.shape[0], c])
+        offs.append(o)
+        data.append(img.reshape(-1))
+        o += img.size
+    return vrt.SceneData(sd.pos, sd.nrm, sd.uv, sd.mat, sd.mat_tex, sd.mat_kd, np.array(dims, np.int32),
+                         np.array(offs, np.int64), np.concatenate(data))
+
+
+def soup(n=2500, seed=5):
+    """Random triangle soup in a box with an untextured and a 1-channel material."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-1, 1, (n, 1, 3))
+    pos = (c + rng.normal(0, 0.08, (n, 3, 3))).astype(np.float32).reshape(n, 9)
+    nrm = rng.normal(0, 1, (n, 9)).astype(np.float32)
+    uv = rng.uniform(-2.5, 3.5, (n, 6)).astype(np.float32)
+    mat = rng.integers(0, 3, n).astype(np.int32)
+    tex = np.concatenate([rng.integers(0, 256, 16 * 12 * 1), rng.integers(0, 256, 8 * 8 * 4)]).astype(np.uint8)
+    return vrt.SceneData(pos, nrm, uv, mat, np.array([0, -1, 1], np.int32),
+                         np.array([[0.2, 0.4, 0.6], [0.9, 0.3, 0.1], [0, 0, 0]], np.float32),
+                         np.array([[16, 12, 1], [8, 8, 4]], np.int32), np.array([0, 192], np.int64), tex)
+
+
+def scene_fixture(name, sd, depth, cams, films):
+    osc = po.Scene(sd, depth)
+    rec = {"pos": sd.pos, "nrm": sd.nrm, "uv": sd.uv, "mat": sd.mat, "mat_tex": sd.mat_tex,
+           "mat_kd": sd.mat_kd, "tex_dims": sd.tex_dims, "tex_off": sd.tex_off, "tex_data": sd.tex_data,
+           "depth": np.int32(depth)}
+    info, box = osc.info()
+    rec["tree_info"] = info
+    rec["root_box"] = box
+    for k, ((fov, eye, spot, up), (fw, fh, nx, ny)) in enumerate(zip(cams, films)):
+        cam = po.camera(fov, eye, spot, up)
+        rgb, so = osc.render(cam, fw, fh, nx, ny, film_index=1, nthreads=8)
+        rec[f"cam{k}"] = np.array([fov, *eye, *spot, *up], np.float32)
+        rec[f"film{k}"] = np.array([fw, fh, nx, ny], np.float32)
+        rec[f"img{k}"] = rgb
+        for key in ("hit", "tri", "voxel", "rgb", "counters"):
+            rec[f"s{k}_{key}"] = so[key]
+    np.savez_compressed(os.path.join(HERE, f"scene_{name}.npz"), **rec)
+    return rec
+
+
+def main():
+    if not po.reference_available():
+        raise SystemExit("oracle/_ref/libvrtref.so missing: run `make` where /root/reference exists")
+    q, out = kat_raytri()
+    np.savez_compressed(os.path.join(HERE, "kat_raytri.npz"), inp=q, out=out)
+    q, out = kat_tribox()
+    np.savez_compressed(os.path.join(HERE, "kat_tribox.npz"), inp=q, out=out)
+    rec = {}
+    for i, img in enumerate(hdr_cases()):
+        rec[f"img{i}"] = img
+        rec[f"bytes{i}"] = np.frombuffer(po.ref_hdr_bytes(img), np.uint8)
+    np.savez_compressed(os.path.join(HERE, "hdr_ref.npz"), **rec)
+
+    main_cam = (vrt.to_radian(90), (1.0, 1.3, -0.2), (0.0, 0.4, 0.0), (0.0, 1.0, 0.0))
+    sd = downsample_textures(vrt.SceneData.proxy(0.02, 1), 8)
+    tree = vrt.VoxelOctree(sd, 6, device=-1)
+    mn, mx = tree.root_box
+    sweep = [(f, tuple(e), tuple(s), tuple(u)) for f, e, s, u in
+             (vrt.sweep_pose(mn, mx, i, 16) for i in (3, 11))]
+    scene_fixture("proxy", sd, 6, [main_cam, sweep[0], sweep[1]],
+                  [(1.0, 1.0, 64, 64), (1.0, 1.0, 48, 32), (1.0, 1.0, 40, 56)])
+    sd2 = soup()
+    scene_fixture("soup", sd2, 7,
+                  [(vrt.to_radian(70), (0.1, 0.2, 2.8), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0)),
+                   (vrt.to_radian(100), (0.05, 0.0, 0.02), (1.0, 0.3, 0.2), (0.0, 1.0, 0.0))],
+                  [(1.0, 1.0, 40, 40), (1.0, 1.0, 33, 27)])
+    for f in sorted(os.listdir(HERE)):
+        print(f, os.path.getsize(os.path.join(HERE, f)))
+
+
+if __name__ == "__main__":
+    main()

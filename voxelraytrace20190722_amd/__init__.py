@@ -1,0 +1,21 @@
+"""MI355X-native drop-in for jqly/VoxelRayTrace20190722's per-pixel
+voxel-octree ray-march + ray/triangle hit loop.
+
+The compute path is libvrt.so (HIP kernels for gfx950 behind the C ABI in
+include/vrt.h); this package is its Python binding.  Importing the API loads
+the library and raises if it is missing: there is no CPU fallback.
+"""
+from ._ffi import VrtError, lib, LIB_PATH  # noqa: F401
+from .api import (  # noqa: F401
+    FLT_MAX, Camera, Film, SceneData, VoxelOctree, device_count, device_selftest,
+    hdr_bytes, intersect_triangle3, make_ray, ray_march, ray_march_init, render,
+    sweep_pose, tiles_per_rank, to_radian, tri_box_overlap, unpack_tiles_device,
+    write_hdr,
+)
+
+__all__ = [
+    "VrtError", "lib", "LIB_PATH", "FLT_MAX", "Camera", "Film", "SceneData", "VoxelOctree",
+    "device_count", "device_selftest", "hdr_bytes", "intersect_triangle3", "make_ray",
+    "ray_march", "ray_march_init", "render", "sweep_pose", "tiles_per_rank", "to_radian",
+    "tri_box_overlap", "unpack_tiles_device", "write_hdr",
+]

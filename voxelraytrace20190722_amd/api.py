@@ -1,0 +1,335 @@
+"""Python mirror of the reference's hot-path interface over libvrt.so.
+
+Names follow the reference (VRT/x = VoxelRayTrace20190722/x):
+  Camera(fov, eye, spot, up, near, far), Camera.gen_rays4/gen_rays1  VRT/camera.h:70-84
+  Film(w, h, nx, ny)                                                 VRT/camera.h:24-39
+  ray_march_init(scene, max_depth) -> VoxelOctree                    VRT/voxel_octree.h:85-86
+  ray_march(tree, rays)                                              VRT/voxel_octree.h:87-89
+  render(tree, cam, film)     the per-pixel loop of VRT/main.cc:118-123 (primary shading)
+  intersect_triangle3 / tri_box_overlap                              VRT/raytri.h:5, tribox2.h:6
+  write_hdr                                                          VRT/stb_image_write.h:178
+Errors raise VrtError (the reference exit()s or returns false).
+"""
+import ctypes as C
+import numpy as np
+
+from . import _ffi
+from ._ffi import VrtError, check, lib, ptr
+
+FLT_MAX = float(np.finfo(np.float32).max)
+
+
+def to_radian(degree):
+    """jql::to_radian: degree * pi / 180.f in float (VRT/graphics_math.h:896-899)."""
+    d = np.float32(degree)
+    return float(np.float32(np.float32(d * np.float32(3.1415926535897932384626)) / np.float32(180.0)))
+
+
+def _f3(v):
+    a = np.ascontiguousarray(np.asarray(v, dtype=np.float32).reshape(3))
+    return a
+
+
+class Film:
+    """Film(w, h, nx, ny) (VRT/camera.h:24-39)."""
+
+    def __init__(self, w, h, nx, ny):
+        self.w, self.h, self.nx, self.ny = float(w), float(h), int(nx), int(ny)
+        self.c = _ffi.Film(self.w, self.h, self.nx, self.ny)
+
+
+class Camera:
+    """Camera(fov, eye, spot, up, near=0, far=FLT_MAX) (VRT/camera.cc:65-75)."""
+
+    def __init__(self, fov, eye, spot, up, near=0.0, far=FLT_MAX):
+        self.c = _ffi.Camera()
+        self.eye, self.spot, self.up = _f3(eye), _f3(spot), _f3(up)
+        check(lib().vrt_camera_init(float(fov), ptr(self.eye, _ffi.f32p), ptr(self.spot, _ffi.f32p),
+                                    ptr(self.up, _ffi.f32p), float(near), float(far),
+                                    C.byref(self.c)), "vrt_camera_init")
+
+    @staticmethod
+    def _rays(arr):
+        out = np.zeros((len(arr), 8), dtype=np.float32)
+        for i, r in enumerate(arr):
+            out[i, 0:3] = r.o[:]
+            out[i, 3:6] = r.d[:]
+            out[i, 6] = r.tmin
+            out[i, 7] = r.tmax
+        return out
+
+    def gen_rays4(self, film, px, py):
+        """4 rays {o, d, tmin, tmax} as a (4, 8) float32 array (VRT/camera.cc:95-112)."""
+        arr = (_ffi.Ray * 4)()
+        check(lib().vrt_gen_rays4(C.byref(self.c), C.byref(film.c), int(px), int(py), arr),
+              "vrt_gen_rays4")
+        return self._rays(arr)
+
+    def gen_rays1(self, film, px, py):
+        arr = (_ffi.Ray * 1)()
+        check(lib().vrt_gen_rays1(C.byref(self.c), C.byref(film.c), int(px), int(py), arr),
+              "vrt_gen_rays1")
+        return self._rays(arr)
+
+
+def make_ray(o, d, tmin=0.0, tmax=FLT_MAX):
+    """jql::Ray(o, d, tmin, tmax): normalises d (VRT/graphics_math.h:1159-1166)."""
+    r = _ffi.Ray()
+    o, d = _f3(o), _f3(d)
+    check(lib().vrt_make_ray(ptr(o, _ffi.f32p), ptr(d, _ffi.f32p), float(tmin), float(tmax),
+                             C.byref(r)), "vrt_make_ray")
+    return np.array(list(r.o) + list(r.d) + [r.tmin, r.tmax], dtype=np.float32)
+
+
+class SceneData:
+    """Triangle soup + materials + textures (the obj2voxel output the
+    reference builds its octree from, VRT/voxel_octree.cc:305-371)."""
+
+    def __init__(self, pos, nrm, uv=None, mat=None, mat_tex=None, mat_kd=None,
+                 tex_dims=None, tex_off=None, tex_data=None):
+        self.pos = np.ascontiguousarray(np.asarray(pos, np.float32).reshape(-1, 9))
+        n = self.pos.shape[0]
+        self.nrm = np.ascontiguousarray(np.asarray(nrm, np.float32).reshape(n, 9))
+        self.uv = None if uv is None else np.ascontiguousarray(np.asarray(uv, np.float32).reshape(n, 6))
+        self.mat = None if mat is None else np.ascontiguousarray(np.asarray(mat, np.int32).reshape(n))
+        self.mat_tex = np.ascontiguousarray(np.asarray([-1] if mat_tex is None else mat_tex, np.int32))
+        self.mat_kd = np.ascontiguousarray(
+            np.asarray([[0.8, 0.8, 0.8]] if mat_kd is None else mat_kd, np.float32).reshape(-1, 3))
+        self.tex_dims = np.ascontiguousarray(np.asarray([] if tex_dims is None else tex_dims,
+                                                        np.int32).reshape(-1, 3))
+        self.tex_off = np.ascontiguousarray(np.asarray([] if tex_off is None else tex_off, np.int64))
+        self.tex_data = np.ascontiguousarray(np.asarray([] if tex_data is None else tex_data, np.uint8))
+
+    @property
+    def ntri(self):
+        return self.pos.shape[0]
+
+    def desc(self):
+        d = _ffi.SceneDesc()
+        d.ntri = self.ntri
+        d.pos = ptr(self.pos, _ffi.f32p)
+        d.nrm = ptr(self.nrm, _ffi.f32p)
+        d.uv = ptr(self.uv, _ffi.f32p)
+        d.mat = ptr(self.mat, _ffi.i32p)
+        d.nmat = len(self.mat_tex)
+        d.mat_tex = ptr(self.mat_tex, _ffi.i32p)
+        d.mat_kd = ptr(self.mat_kd, _ffi.f32p)
+        d.ntex = len(self.tex_off)
+        d.tex_dims = ptr(self.tex_dims, _ffi.i32p) if len(self.tex_off) else None
+        d.tex_off = ptr(self.tex_off, _ffi.i64p) if len(self.tex_off) else None
+        d.tex_data = ptr(self.tex_data, _ffi.u8p) if len(self.tex_off) else None
+        d.tex_bytes = int(self.tex_data.size)
+        return d
+
+    @classmethod
+    def proxy(cls, detail=1.0, seed=1):
+        """The deterministic sponza-proxy atrium (vrt_proxy_scene)."""
+        L = lib()
+        nt, nm, nx, tb = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+        check(L.vrt_proxy_scene(float(detail), int(seed), C.byref(nt), None, None, None, None,
+                                C.byref(nm), None, None, C.byref(nx), None, None, None,
+                                C.byref(tb)), "vrt_proxy_scene(count)")
+        n = nt.value
+        pos = np.zeros((n, 9), np.float32)
+        nrm = np.zeros((n, 9), np.float32)
+        uv = np.zeros((n, 6), np.float32)
+        mat = np.zeros(n, np.int32)
+        mt = np.zeros(nm.value, np.int32)
+        kd = np.zeros((nm.value, 3), np.float32)
+        td = np.zeros((nx.value, 3), np.int32)
+        to = np.zeros(nx.value, np.int64)
+        tx = np.zeros(tb.value, np.uint8)
+        check(L.vrt_proxy_scene(float(detail), int(seed), C.byref(nt), ptr(pos, _ffi.f32p),
+                                ptr(nrm, _ffi.f32p), ptr(uv, _ffi.f32p), ptr(mat, _ffi.i32p),
+                                C.byref(nm), ptr(mt, _ffi.i32p), ptr(kd, _ffi.f32p), C.byref(nx),
+                                ptr(td, _ffi.i32p), ptr(to, _ffi.i64p), ptr(tx, _ffi.u8p),
+                                C.byref(tb)), "vrt_proxy_scene")
+        return cls(pos, nrm, uv, mat, mt, kd, td, to, tx)
+
+
+class VoxelOctree:
+    """The octree built by gi::ray_march_init and resident on one device
+    (device < 0: host-only, for inspecting the build)."""
+
+    def __init__(self, scene, max_depth, device=0):
+        self.scene = scene  # keeps the arrays alive for the descriptor
+        h = C.c_void_p()
+        d = scene.desc()
+        check(lib().vrt_scene_create(C.byref(d), int(max_depth), int(device), C.byref(h)),
+              "vrt_scene_create")
+        self.h = h
+        self.max_depth = int(max_depth)
+        self.info = _ffi.SceneInfo()
+        check(lib().vrt_scene_info(self.h, C.byref(self.info)), "vrt_scene_info")
+
+    def close(self):
+        if self.h:
+            lib().vrt_scene_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def root_box(self):
+        return (np.array(self.info.root_min[:], np.float32), np.array(self.info.root_max[:], np.float32))
+
+    def leaves(self):
+        """(voxel ids, counts, concatenated triangle lists) of the non-empty leaves."""
+        nl, nr = self.info.nonempty_leaves, self.info.tri_refs
+        vox = np.zeros(nl, np.uint32)
+        cnt = np.zeros(nl, np.uint32)
+        tris = np.zeros(max(nr, 1), np.int32)
+        check(lib().vrt_scene_leaves(self.h, ptr(vox, _ffi.u32p), ptr(cnt, _ffi.u32p),
+                                     ptr(tris, _ffi.i32p)), "vrt_scene_leaves")
+        return vox, cnt, tris[:nr]
+
+    def ray_march(self, rays):
+        """Batched gi::ray_march over (n, 8) rays {o, d, tmin, tmax} (d normalised)."""
+        rays = np.ascontiguousarray(np.asarray(rays, np.float32).reshape(-1, 8))
+        n = rays.shape[0]
+        out = np.zeros((max(n, 1), 9), np.uint32)
+        check(lib().vrt_ray_march_batch(self.h, rays.ctypes.data_as(C.POINTER(_ffi.Ray)), n,
+                                        out.ctypes.data_as(C.POINTER(_ffi.Hit))),
+              "vrt_ray_march_batch")
+        out = out[:n]
+        return {"hit": out[:, 0].astype(np.int32), "tri": out[:, 1].view(np.int32).copy(),
+                "voxel": out[:, 2].copy(), "hit_p": out[:, 3:6].view(np.float32).copy(),
+                "normal": out[:, 6:9].view(np.float32).copy()}
+
+    def render(self, cam, film, samples=False, counters=False):
+        """Primary render -> (ny, nx, 3) float32 image (+ per-sample dict)."""
+        nx, ny = film.nx, film.ny
+        rgb = np.zeros((ny, nx, 3), np.float32)
+        smp = None
+        st = None
+        so = None
+        if samples or counters:
+            ns = nx * ny * 4
+            so = {}
+            s = _ffi.Samples()
+            if samples:
+                so["hit"] = np.zeros(ns, np.int32)
+                so["tri"] = np.zeros(ns, np.int32)
+                so["voxel"] = np.zeros(ns, np.uint32)
+                so["rgb"] = np.zeros((ns, 3), np.float32)
+                s.hit = ptr(so["hit"], _ffi.i32p)
+                s.tri = ptr(so["tri"], _ffi.i32p)
+                s.voxel = ptr(so["voxel"], _ffi.u32p)
+                s.rgb = ptr(so["rgb"], _ffi.f32p)
+            if counters:
+                so["counters"] = np.zeros((ns, 4), np.uint32)
+                s.counters = ptr(so["counters"], _ffi.u32p)
+                st = _ffi.Stats()
+            smp = C.byref(s)
+        check(lib().vrt_render(self.h, C.byref(cam.c), C.byref(film.c), ptr(rgb, _ffi.f32p), smp,
+                               C.byref(st) if st is not None else None), "vrt_render")
+        if so is not None and st is not None:
+            so["stats"] = {"rays": st.rays, "aabb_tests": st.aabb_tests, "leaves": st.leaves,
+                           "tri_tests": st.tri_tests, "hits": st.hits, "kernel_ms": st.kernel_ms}
+        return (rgb, so) if so is not None else rgb
+
+    def render_tiles_device(self, cam, film, rank, nranks, image_layout, d_out_ptr, stream_ptr=None):
+        check(lib().vrt_render_tiles_device(self.h, C.byref(cam.c), C.byref(film.c), int(rank),
+                                            int(nranks), int(image_layout), C.c_void_p(d_out_ptr),
+                                            C.c_void_p(stream_ptr) if stream_ptr else None),
+              "vrt_render_tiles_device")
+
+    def last_kernel_ms(self):
+        ms = C.c_float()
+        check(lib().vrt_last_kernel_ms(self.h, C.byref(ms)), "vrt_last_kernel_ms")
+        return ms.value
+
+
+def ray_march_init(scene, max_depth, device=0):
+    """gi::ray_march_init(root, voxels, max_depth) (VRT/voxel_octree.cc:67-75)."""
+    return VoxelOctree(scene, max_depth, device)
+
+
+def ray_march(tree, rays):
+    """gi::ray_march over a batch of rays (VRT/voxel_octree.cc:131-188)."""
+    return tree.ray_march(rays)
+
+
+def render(tree, cam, film, **kw):
+    return tree.render(cam, film, **kw)
+
+
+def tiles_per_rank(film, nranks):
+    return lib().vrt_tiles_per_rank(C.byref(film.c), int(nranks))
+
+
+def unpack_tiles_device(film, nranks, d_gathered_ptr, d_image_ptr, stream_ptr=None):
+    check(lib().vrt_unpack_tiles_device(C.byref(film.c), int(nranks), C.c_void_p(d_gathered_ptr),
+                                        C.c_void_p(d_image_ptr),
+                                        C.c_void_p(stream_ptr) if stream_ptr else None),
+          "vrt_unpack_tiles_device")
+
+
+def intersect_triangle3(orig, direction, v0, v1, v2):
+    """VRT/raytri.h:5-7 -> (ret, t, u, v); t/u/v only meaningful when ret == 1."""
+    a = [np.ascontiguousarray(np.asarray(x, np.float64).reshape(3)) for x in (orig, direction, v0, v1, v2)]
+    t, u, v = C.c_double(), C.c_double(), C.c_double()
+    r = lib().intersect_triangle3(*[ptr(x, _ffi.f64p) for x in a], C.byref(t), C.byref(u), C.byref(v))
+    return r, t.value, u.value, v.value
+
+
+def tri_box_overlap(center, half, tri):
+    """VRT/tribox2.h:6 -> 1/0."""
+    c = np.ascontiguousarray(np.asarray(center, np.float32).reshape(3))
+    h = np.ascontiguousarray(np.asarray(half, np.float32).reshape(3))
+    t = np.ascontiguousarray(np.asarray(tri, np.float32).reshape(9))
+    return lib().triBoxOverlap(ptr(c, _ffi.f32p), ptr(h, _ffi.f32p), ptr(t, _ffi.f32p))
+
+
+def hdr_bytes(img):
+    """The exact bytes stbi_write_hdr would write for img (h, w, comp)."""
+    img = np.ascontiguousarray(np.asarray(img, np.float32))
+    h, w = img.shape[:2]
+    comp = 1 if img.ndim == 2 else img.shape[2]
+    n = lib().vrt_write_hdr_mem(w, h, comp, ptr(img, _ffi.f32p), None, 0)
+    if n == 0:
+        raise VrtError(_ffi.VRT_E_INVALID, "vrt_write_hdr_mem")
+    buf = np.zeros(-n, np.uint8)
+    n2 = lib().vrt_write_hdr_mem(w, h, comp, ptr(img, _ffi.f32p), ptr(buf, _ffi.u8p), -n)
+    assert n2 == -n
+    return buf.tobytes()
+
+
+def write_hdr(path, img):
+    """stbi_write_hdr(path, w, h, comp, data): True on success."""
+    img = np.ascontiguousarray(np.asarray(img, np.float32))
+    h, w = img.shape[:2]
+    comp = 1 if img.ndim == 2 else img.shape[2]
+    return lib().vrt_write_hdr(str(path).encode(), w, h, comp, ptr(img, _ffi.f32p)) == 1
+
+
+def sweep_pose(root_min, root_max, i, n):
+    """Camera-sweep pose i of n -> (fov, eye, spot, up)."""
+    mn, mx = _f3(root_min), _f3(root_max)
+    eye, spot, up = np.zeros(3, np.float32), np.zeros(3, np.float32), np.zeros(3, np.float32)
+    fov = C.c_float()
+    check(lib().vrt_sweep_pose(ptr(mn, _ffi.f32p), ptr(mx, _ffi.f32p), int(i), int(n), ptr(eye, _ffi.f32p),
+                               ptr(spot, _ffi.f32p), ptr(up, _ffi.f32p), C.byref(fov)), "vrt_sweep_pose")
+    return fov.value, eye, spot, up
+
+
+def device_count():
+    n = C.c_int32()
+    check(lib().vrt_device_count(C.byref(n)), "vrt_device_count")
+    return n.value
+
+
+def device_selftest(mt_in=None, sat_in=None, device=0):
+    """Run the kernels' own MT / SAT code on the device over n cases."""
+    n = len(mt_in) if mt_in is not None else len(sat_in)
+    mt_out = np.zeros((n, 4), np.float64) if mt_in is not None else None
+    sat_out = np.zeros(n, np.int32) if sat_in is not None else None
+    mi = None if mt_in is None else np.ascontiguousarray(np.asarray(mt_in, np.float64).reshape(n, 15))
+    si = None if sat_in is None else np.ascontiguousarray(np.asarray(sat_in, np.float32).reshape(n, 15))
+    check(lib().vrt_device_selftest(int(device), ptr(mi, _ffi.f64p), ptr(mt_out, _ffi.f64p),
+                                    ptr(si, _ffi.f32p), ptr(sat_out, _ffi.i32p), n), "vrt_device_selftest")
+    return mt_out, sat_out

@@ -1,0 +1,985 @@
+// vrt_host.cpp -- host side of libvrt.so: the C ABI of include/vrt.h.
+//
+//  * octree build (gi::ray_march_init, VRT/voxel_octree.cc:27-75) as a
+//    parallel per-triangle descent + sort, flattened to the BFS child-block
+//    layout the kernels read (DESIGN.md "Data layout in HBM");
+//  * scene upload, render / ray-march orchestration on a HIP stream;
+//  * camera (VRT/camera.cc:65-112) and the legacy intersect_triangle3 /
+//    triBoxOverlap symbols, all through vrt_math.h (the kernels' own code).
+//
+// VRT/x = /root/reference/VoxelRayTrace20190722/x
+#include "../../include/vrt.h"
+#include "vrt_internal.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+using namespace vrt;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int fail(int code, const char *fmt, ...)
+{
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        g_err = buf;
+        return code;
+}
+
+#define HIPCHK(expr)                                                             \
+        do {                                                                     \
+                hipError_t e_ = (expr);                                          \
+                if (e_ != hipSuccess)                                            \
+                        return fail(VRT_E_DEVICE, "%s failed: %s", #expr,       \
+                                    hipGetErrorString(e_));                      \
+        } while (0)
+
+extern "C" const char *vrt_last_error(void) { return g_err.c_str(); }
+
+extern "C" const char *vrt_status_string(int s)
+{
+        switch (s) {
+        case VRT_OK: return "ok";
+        case VRT_E_INVALID: return "invalid argument";
+        case VRT_E_NOMEM: return "out of host memory";
+        case VRT_E_DEVICE: return "HIP runtime error";
+        case VRT_E_NODEVICE: return "no usable gfx950 device";
+        case VRT_E_IO: return "i/o error";
+        default: return "unknown status";
+        }
+}
+
+static double now_ms()
+{
+        using namespace std::chrono;
+        return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+// ---------------------------------------------------------------------------
+// legacy reference symbols
+// ---------------------------------------------------------------------------
+extern "C" int intersect_triangle3(double orig[3], double dir[3],
+                                   double vert0[3], double vert1[3],
+                                   double vert2[3], double *t, double *u,
+                                   double *v)
+{
+        return mt_isect(orig, dir, vert0, vert1, vert2, t, u, v);
+}
+
+extern "C" int triBoxOverlap(float boxcenter[3], float boxhalfsize[3],
+                             float triverts[3][3])
+{
+        return tri_box_overlap(boxcenter, boxhalfsize, &triverts[0][0]);
+}
+
+// ---------------------------------------------------------------------------
+// camera (VRT/camera.cc:65-112)
+// ---------------------------------------------------------------------------
+extern "C" int vrt_camera_init(float fov, const float eye[3],
+                               const float spot[3], const float up[3],
+                               float near_, float far_, vrt_camera *out)
+{
+        if (!eye || !spot || !up || !out)
+                return fail(VRT_E_INVALID, "vrt_camera_init: null argument");
+        const f3 e = mk3(eye[0], eye[1], eye[2]);
+        const f3 fwd = normalize(mk3(spot[0], spot[1], spot[2]) - e);
+        const f3 s = normalize(cross(fwd, mk3(up[0], up[1], up[2])));
+        const f3 u = normalize(cross(s, fwd));
+        const f3 nf = -fwd;
+        const float C[16] = { s.x, s.y, s.z, 0.f, u.x, u.y, u.z, 0.f,
+                              nf.x, nf.y, nf.z, 0.f, e.x, e.y, e.z, 1.f };
+        std::memcpy(out->C, C, sizeof C);
+        out->fov = fov;
+        out->near_ = near_;
+        out->far_ = far_;
+        // point_transform(C_, {}): dot(C, (0,0,0,1)) then /= w
+        // (VRT/graphics_math.h:1063-1070)
+        float r[4];
+        for (int k = 0; k < 4; ++k) {
+                float acc = 0.0f;
+                acc += C[k] * 0.0f;
+                acc += C[4 + k] * 0.0f;
+                acc += C[8 + k] * 0.0f;
+                acc += C[12 + k] * 1.0f;
+                r[k] = acc;
+        }
+        const float w = r[3];
+        for (int k = 0; k < 3; ++k)
+                out->origin[k] = r[k] / w;
+        return VRT_OK;
+}
+
+static float cam_zplane(const vrt_camera *cam, const vrt_film *film)
+{
+        // -(film.h / (2 * std::tanf(fov / 2)))  (VRT/camera.cc:100)
+        return -(film->h / (2.0f * tanf(cam->fov / 2.0f)));
+}
+
+static void fill_cam_params(const vrt_camera *cam, const vrt_film *film,
+                            CamParams *cp)
+{
+        for (int k = 0; k < 3; ++k) {
+                cp->s[k] = cam->C[k];
+                cp->u[k] = cam->C[4 + k];
+                cp->nf[k] = cam->C[8 + k];
+                cp->e[k] = cam->C[12 + k];
+                cp->origin[k] = cam->origin[k];
+        }
+        cp->z = cam_zplane(cam, film);
+        cp->tmin = cam->near_;
+        cp->tmax = cam->far_;
+        cp->nx = film->nx;
+        cp->ny = film->ny;
+}
+
+static int gen_rays(const vrt_camera *cam, const vrt_film *film, int px,
+                    int py, vrt_ray *out, int n)
+{
+        if (!cam || !film || !out)
+                return fail(VRT_E_INVALID, "gen_rays: null argument");
+        if (px < 0 || px >= film->nx || py < 0 || py >= film->ny)
+                return fail(VRT_E_INVALID, "gen_rays: pixel (%d,%d) outside film", px, py);
+        CamParams cp;
+        fill_cam_params(cam, film, &cp);
+        for (int s = 0; s < n; ++s) {
+                const float sx = n == 4 ? sample_x(s) : 0.5f;
+                const float sy = n == 4 ? sample_y(s) : 0.5f;
+                const f3 d = camera_dir(cp.s, cp.u, cp.nf, cp.e, cp.z, cp.nx, cp.ny,
+                                        px, py, sx, sy);
+                for (int k = 0; k < 3; ++k)
+                        out[s].o[k] = cp.origin[k];
+                out[s].d[0] = d.x;
+                out[s].d[1] = d.y;
+                out[s].d[2] = d.z;
+                out[s].tmin = cp.tmin;
+                out[s].tmax = cp.tmax;
+        }
+        return VRT_OK;
+}
+
+extern "C" int vrt_gen_rays4(const vrt_camera *cam, const vrt_film *film,
+                             int px, int py, vrt_ray out[4])
+{
+        return gen_rays(cam, film, px, py, out, 4);
+}
+
+extern "C" int vrt_gen_rays1(const vrt_camera *cam, const vrt_film *film,
+                             int px, int py, vrt_ray out[1])
+{
+        return gen_rays(cam, film, px, py, out, 1);
+}
+
+extern "C" int vrt_make_ray(const float o[3], const float d[3], float tmin,
+                            float tmax, vrt_ray *out)
+{
+        if (!o || !d || !out)
+                return fail(VRT_E_INVALID, "vrt_make_ray: null argument");
+        const f3 dn = normalize(mk3(d[0], d[1], d[2]));
+        for (int k = 0; k < 3; ++k)
+                out->o[k] = o[k];
+        out->d[0] = dn.x;
+        out->d[1] = dn.y;
+        out->d[2] = dn.z;
+        out->tmin = tmin;
+        out->tmax = tmax;
+        return VRT_OK;
+}
+
+extern "C" int vrt_aabb_isect(const float box[6], const vrt_ray *ray)
+{
+        if (!box || !ray)
+                return 0;
+        const f3 o = mk3(ray->o[0], ray->o[1], ray->o[2]);
+        const f3 di = mk3(dinv_of(ray->d[0]), dinv_of(ray->d[1]), dinv_of(ray->d[2]));
+        return aabb_isect(box, box + 3, o, di, ray->tmin, ray->tmax) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// octree build
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Box {
+        float mn[3], mx[3];
+};
+
+// split() child box (VRT/voxel_octree.cc:30-35)
+inline Box child_box(const Box &p, int i)
+{
+        Box c;
+        const int m[3] = { (i & 4) ? 1 : 0, (i & 2) ? 1 : 0, (i & 1) ? 1 : 0 };
+        for (int k = 0; k < 3; ++k) {
+                const float half = (p.mx[k] - p.mn[k]) / 2.0f;
+                c.mn[k] = p.mn[k] + (float)m[k] * half;
+                c.mx[k] = c.mn[k] + half;
+        }
+        return c;
+}
+
+// Triangle::is_overlap (VRT/voxel_octree.cc:486-492)
+inline bool overlaps(const float *tri9, const Box &b)
+{
+        float c[3], h[3];
+        for (int k = 0; k < 3; ++k) {
+                c[k] = (b.mn[k] + b.mx[k]) * .5f;
+                h[k] = (b.mx[k] - b.mn[k]) / 2.f;
+        }
+        return tri_box_overlap(c, h, tri9) == 1;
+}
+
+struct BuildOut {
+        // internal node keys per depth (path code, 3 bits per level)
+        std::vector<std::vector<uint32_t>> internal;
+        // (leaf code << 32 | tri) at max depth
+        std::vector<uint64_t> refs;
+};
+
+// Descend one triangle: the set of nodes insert() reaches for it.  A node is
+// split iff some triangle overlaps it (and all its ancestors) above
+// max_depth; a max-depth leaf lists exactly those triangles.
+void descend(const float *tri9, uint32_t tri, const Box &b, int depth,
+             int max_depth, uint32_t code, BuildOut &o)
+{
+        if (!overlaps(tri9, b))
+                return;
+        if (depth == max_depth) {
+                o.refs.push_back(((uint64_t)code << 32) | tri);
+                return;
+        }
+        o.internal[depth].push_back(code);
+        for (int i = 0; i < 8; ++i)
+                descend(tri9, tri, child_box(b, i), depth + 1, max_depth,
+                        (code << 3) | (uint32_t)i, o);
+}
+
+uint32_t vox_of(uint32_t code, int depth)
+{
+        uint32_t ix = 0, iy = 0, iz = 0;
+        for (int l = depth - 2; l >= 0; --l) {
+                const uint32_t ci = (code >> (3 * l)) & 7u;
+                ix = (ix << 1) | ((ci >> 2) & 1u);
+                iy = (iy << 1) | ((ci >> 1) & 1u);
+                iz = (iz << 1) | (ci & 1u);
+        }
+        return ix | (iy << 10) | (iz << 20);
+}
+
+}  // namespace
+
+struct vrt_scene {
+        int device = 0;
+        int max_depth = 0;
+        int ntri = 0;
+        std::vector<NodeRec> nodes;
+        std::vector<uint32_t> node_vox;
+        std::vector<RefRec> refs;
+        std::vector<TriPos> tri_pos;
+        std::vector<TriAttr> tri_attr;
+        std::vector<MatRec> mats;
+        std::vector<TexRec> texs;
+        int64_t tex_bytes = 0;
+        vrt_scene_info_t info{};
+        // device
+        void *d_mem = nullptr;
+        DevScene dev{};
+        hipStream_t stream = nullptr;
+        hipEvent_t ev0 = nullptr, ev1 = nullptr;
+        bool timed = false;
+        std::mutex mu;
+};
+
+static int build_tree(vrt_scene *s, const vrt_scene_desc *d)
+{
+        const int D = s->max_depth;
+        const int n = d->ntri;
+        // root = AABB{} merged with every triangle AABB, in input order
+        // (VRT/voxel_octree.cc:70-72; AABB(Iter,Iter) graphics_math.h:1240-1251)
+        Box root;
+        for (int k = 0; k < 3; ++k) {
+                root.mn[k] = kFltMax;
+                root.mx[k] = -kFltMax;
+        }
+        for (int i = 0; i < n; ++i) {
+                const float *p = d->pos + 9 * (size_t)i;
+                float tmn[3] = { kFltMax, kFltMax, kFltMax };
+                float tmx[3] = { -kFltMax, -kFltMax, -kFltMax };
+                for (int v = 0; v < 3; ++v)
+                        for (int k = 0; k < 3; ++k) {
+                                tmn[k] = std_min(tmn[k], p[3 * v + k]);
+                                tmx[k] = std_max(tmx[k], p[3 * v + k]);
+                        }
+                for (int k = 0; k < 3; ++k) {
+                        root.mn[k] = std_min(root.mn[k], tmn[k]);
+                        root.mx[k] = std_max(root.mx[k], tmx[k]);
+                }
+        }
+
+        // parallel per-triangle descent
+        unsigned nth = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+        if (n < 4096)
+                nth = 1;
+        std::vector<BuildOut> outs(nth);
+        for (auto &o : outs)
+                o.internal.resize(D + 1);
+        {
+                std::atomic<int> next{ 0 };
+                auto work = [&](unsigned t) {
+                        BuildOut &o = outs[t];
+                        for (;;) {
+                                const int i0 = next.fetch_add(1024);
+                                if (i0 >= n)
+                                        break;
+                                const int i1 = std::min(n, i0 + 1024);
+                                for (int i = i0; i < i1; ++i)
+                                        descend(d->pos + 9 * (size_t)i, (uint32_t)i, root, 1, D, 0u, o);
+                        }
+                };
+                std::vector<std::thread> th;
+                for (unsigned t = 1; t < nth; ++t)
+                        th.emplace_back(work, t);
+                work(0);
+                for (auto &x : th)
+                        x.join();
+        }
+        // merge
+        std::vector<std::vector<uint32_t>> internal(D + 1);
+        for (int l = 1; l < D; ++l) {
+                size_t tot = 0;
+                for (auto &o : outs)
+                        tot += o.internal[l].size();
+                internal[l].reserve(tot);
+                for (auto &o : outs) {
+                        internal[l].insert(internal[l].end(), o.internal[l].begin(), o.internal[l].end());
+                        std::vector<uint32_t>().swap(o.internal[l]);
+                }
+                std::sort(internal[l].begin(), internal[l].end());
+                internal[l].erase(std::unique(internal[l].begin(), internal[l].end()), internal[l].end());
+        }
+        std::vector<uint64_t> refs;
+        {
+                size_t tot = 0;
+                for (auto &o : outs)
+                        tot += o.refs.size();
+                refs.reserve(tot);
+                for (auto &o : outs) {
+                        refs.insert(refs.end(), o.refs.begin(), o.refs.end());
+                        std::vector<uint64_t>().swap(o.refs);
+                }
+                // (leaf code, tri index): leaf lists in insertion = input order
+                std::sort(refs.begin(), refs.end());
+        }
+
+        // flatten: root = node 0; level by level, internal nodes in code
+        // order each own the next block of 8 children.
+        int64_t ninternal = 0;
+        for (int l = 1; l < D; ++l)
+                ninternal += (int64_t)internal[l].size();
+        const int64_t nnodes = 1 + 8 * ninternal;
+        if (nnodes > 0x7FFFFFFF)
+                return fail(VRT_E_INVALID, "octree too large (%lld nodes)", (long long)nnodes);
+        s->nodes.assign((size_t)nnodes, NodeRec{});
+        s->node_vox.assign((size_t)nnodes, 0u);
+        s->refs.resize(refs.size());
+        std::vector<Box> boxes((size_t)nnodes);
+        std::vector<uint32_t> codes((size_t)nnodes);
+        std::vector<int32_t> depth_of((size_t)nnodes);
+        boxes[0] = root;
+        codes[0] = 0;
+        depth_of[0] = 1;
+        // first node index of each level and the block base of each internal
+        // node: internal node j (global order) owns children 1 + 8j ...
+        int64_t j_base = 0;  // global index of first internal node at level l
+        // level l's nodes occupy a contiguous index range [lv_begin, lv_end)
+        int64_t lv_begin = 0, lv_end = 1;
+        size_t ref_pos = 0;
+        for (int l = 1; l <= D; ++l) {
+                const std::vector<uint32_t> &I = internal[l];  // empty at l == D
+                // nodes of this level are in code order (children blocks of
+                // the previous level's code-ordered internal nodes)
+                size_t ii = 0;
+                for (int64_t ni = lv_begin; ni < lv_end; ++ni) {
+                        const uint32_t code = codes[ni];
+                        NodeRec &nr = s->nodes[ni];
+                        for (int k = 0; k < 3; ++k) {
+                                nr.bmin[k] = boxes[ni].mn[k];
+                                nr.bmax[k] = boxes[ni].mx[k];
+                        }
+                        s->node_vox[ni] = vox_of(code, l);
+                        while (ii < I.size() && I[ii] < code)
+                                ++ii;
+                        if (l < D && ii < I.size() && I[ii] == code) {
+                                const int64_t jg = j_base + (int64_t)ii;
+                                const int64_t first = 1 + 8 * jg;
+                                nr.a = (uint32_t)first;
+                                nr.b = 0;
+                                for (int c = 0; c < 8; ++c) {
+                                        boxes[first + c] = child_box(boxes[ni], c);
+                                        codes[first + c] = (code << 3) | (uint32_t)c;
+                                        depth_of[first + c] = l + 1;
+                                }
+                        } else if (l == D) {
+                                // max-depth leaf: its list in refs
+                                const uint64_t key = (uint64_t)code << 32;
+                                while (ref_pos < refs.size() && refs[ref_pos] < key)
+                                        ++ref_pos;
+                                const size_t r0 = ref_pos;
+                                while (ref_pos < refs.size() && (refs[ref_pos] >> 32) == code)
+                                        ++ref_pos;
+                                nr.a = kLeafBit | (uint32_t)(ref_pos - r0);
+                                nr.b = (uint32_t)r0;
+                        } else {
+                                nr.a = kLeafBit;  // empty leaf above max depth
+                                nr.b = 0;
+                        }
+                }
+                // next level: children of this level's internal nodes, in
+                // the same (code) order
+                const int64_t next_begin = lv_end;
+                const int64_t next_end = next_begin + 8 * (int64_t)I.size();
+                j_base += (int64_t)I.size();
+                lv_begin = next_begin;
+                lv_end = next_end;
+                if (l < D && lv_begin == lv_end)
+                        break;
+        }
+        for (size_t i = 0; i < refs.size(); ++i) {
+                const uint32_t t = (uint32_t)(refs[i] & 0xFFFFFFFFu);
+                RefRec &rr = s->refs[i];
+                std::memcpy(rr.p, d->pos + 9 * (size_t)t, sizeof rr.p);
+                rr.tri = t;
+                rr.pad[0] = rr.pad[1] = 0;
+        }
+        int64_t leaves = 0, nonempty = 0;
+        for (const NodeRec &nr : s->nodes) {
+                if (nr.a & kLeafBit) {
+                        ++leaves;
+                        if (nr.a & ~kLeafBit)
+                                ++nonempty;
+                }
+        }
+        s->info.nodes = nnodes;
+        s->info.internal = ninternal;
+        s->info.leaves = leaves;
+        s->info.nonempty_leaves = nonempty;
+        s->info.tri_refs = (int64_t)refs.size();
+        for (int k = 0; k < 3; ++k) {
+                s->info.root_min[k] = root.mn[k];
+                s->info.root_max[k] = root.mx[k];
+        }
+        return VRT_OK;
+}
+
+static int check_device(int device)
+{
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+                return fail(VRT_E_NODEVICE, "no HIP device visible");
+        if (device < 0 || device >= n)
+                return fail(VRT_E_NODEVICE, "device %d out of range (%d visible)", device, n);
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, device));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+                return fail(VRT_E_NODEVICE, "device %d is %s, kernels are built for gfx950",
+                            device, prop.gcnArchName);
+        return VRT_OK;
+}
+
+extern "C" int vrt_device_count(int *n)
+{
+        if (!n)
+                return fail(VRT_E_INVALID, "null");
+        *n = 0;
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess)
+                return VRT_OK;
+        *n = c;
+        return VRT_OK;
+}
+
+static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int upload(vrt_scene *s, const vrt_scene_desc *d)
+{
+        int rc = check_device(s->device);
+        if (rc)
+                return rc;
+        HIPCHK(hipSetDevice(s->device));
+        const size_t sz_nodes = s->nodes.size() * sizeof(NodeRec);
+        const size_t sz_vox = s->node_vox.size() * sizeof(uint32_t);
+        const size_t sz_refs = std::max<size_t>(1, s->refs.size()) * sizeof(RefRec);
+        const size_t sz_pos = std::max<size_t>(1, s->tri_pos.size()) * sizeof(TriPos);
+        const size_t sz_attr = std::max<size_t>(1, s->tri_attr.size()) * sizeof(TriAttr);
+        const size_t sz_mats = s->mats.size() * sizeof(MatRec);
+        const size_t sz_texs = std::max<size_t>(1, s->texs.size()) * sizeof(TexRec);
+        const size_t sz_tex = (size_t)std::max<int64_t>(16, s->tex_bytes);
+        size_t off[9];
+        size_t tot = 0;
+        const size_t sizes[8] = { sz_nodes, sz_vox, sz_refs, sz_pos, sz_attr, sz_mats, sz_texs, sz_tex };
+        for (int i = 0; i < 8; ++i) {
+                off[i] = tot;
+                tot += align_up(sizes[i]);
+        }
+        off[8] = tot;
+        HIPCHK(hipMalloc(&s->d_mem, tot));
+        char *base = static_cast<char *>(s->d_mem);
+        HIPCHK(hipMemcpy(base + off[0], s->nodes.data(), sz_nodes, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(base + off[1], s->node_vox.data(), sz_vox, hipMemcpyHostToDevice));
+        if (!s->refs.empty())
+                HIPCHK(hipMemcpy(base + off[2], s->refs.data(), s->refs.size() * sizeof(RefRec), hipMemcpyHostToDevice));
+        if (!s->tri_pos.empty())
+                HIPCHK(hipMemcpy(base + off[3], s->tri_pos.data(), s->tri_pos.size() * sizeof(TriPos), hipMemcpyHostToDevice));
+        if (!s->tri_attr.empty())
+                HIPCHK(hipMemcpy(base + off[4], s->tri_attr.data(), s->tri_attr.size() * sizeof(TriAttr), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(base + off[5], s->mats.data(), sz_mats, hipMemcpyHostToDevice));
+        if (!s->texs.empty())
+                HIPCHK(hipMemcpy(base + off[6], s->texs.data(), s->texs.size() * sizeof(TexRec), hipMemcpyHostToDevice));
+        if (s->tex_bytes > 0)
+                HIPCHK(hipMemcpy(base + off[7], d->tex_data, (size_t)s->tex_bytes, hipMemcpyHostToDevice));
+        s->dev.nodes = reinterpret_cast<const NodeRec *>(base + off[0]);
+        s->dev.node_vox = reinterpret_cast<const uint32_t *>(base + off[1]);
+        s->dev.refs = reinterpret_cast<const RefRec *>(base + off[2]);
+        s->dev.tri_pos = reinterpret_cast<const TriPos *>(base + off[3]);
+        s->dev.tri_attr = reinterpret_cast<const TriAttr *>(base + off[4]);
+        s->dev.mats = reinterpret_cast<const MatRec *>(base + off[5]);
+        s->dev.texs = reinterpret_cast<const TexRec *>(base + off[6]);
+        s->dev.tex_data = reinterpret_cast<const uint8_t *>(base + off[7]);
+        s->dev.max_depth = s->max_depth;
+        s->dev.nmat = (int32_t)s->mats.size();
+        s->dev.ntex = (int32_t)s->texs.size();
+        s->info.device_bytes = (int64_t)tot;
+        HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreate(&s->ev0));
+        HIPCHK(hipEventCreate(&s->ev1));
+        return VRT_OK;
+}
+
+static int validate_desc(const vrt_scene_desc *d, int max_depth)
+{
+        if (!d)
+                return fail(VRT_E_INVALID, "null scene descriptor");
+        if (max_depth < 1 || max_depth > VRT_MAX_DEPTH)
+                return fail(VRT_E_INVALID, "max_depth %d outside [1,%d]", max_depth, VRT_MAX_DEPTH);
+        if (d->ntri < 0 || (d->ntri > 0 && (!d->pos || !d->nrm)))
+                return fail(VRT_E_INVALID, "bad triangle arrays");
+        if (d->nmat < 1 || !d->mat_tex || !d->mat_kd)
+                return fail(VRT_E_INVALID, "need >= 1 material (mat_tex, mat_kd)");
+        if (d->ntex < 0 || (d->ntex > 0 && (!d->tex_dims || !d->tex_off || !d->tex_data)))
+                return fail(VRT_E_INVALID, "bad texture arrays");
+        for (int m = 0; m < d->nmat; ++m)
+                if (d->mat_tex[m] < -1 || d->mat_tex[m] >= d->ntex)
+                        return fail(VRT_E_INVALID, "material %d: texture id %d out of range", m, d->mat_tex[m]);
+        for (int t = 0; t < d->ntex; ++t) {
+                const int w = d->tex_dims[3 * t], h = d->tex_dims[3 * t + 1], c = d->tex_dims[3 * t + 2];
+                if (w < 1 || h < 1 || c < 1 || c > 4 || d->tex_off[t] < 0 ||
+                    d->tex_off[t] + (int64_t)w * h * c > d->tex_bytes)
+                        return fail(VRT_E_INVALID, "texture %d: bad dims/offset", t);
+        }
+        if (d->mat)
+                for (int i = 0; i < d->ntri; ++i)
+                        if (d->mat[i] < 0 || d->mat[i] >= d->nmat)
+                                return fail(VRT_E_INVALID, "triangle %d: material %d out of range", i, d->mat[i]);
+        return VRT_OK;
+}
+
+extern "C" int vrt_scene_create(const vrt_scene_desc *d, int max_depth,
+                                int device, vrt_scene **out)
+{
+        if (!out)
+                return fail(VRT_E_INVALID, "null out");
+        *out = nullptr;
+        int rc = validate_desc(d, max_depth);
+        if (rc)
+                return rc;
+        std::unique_ptr<vrt_scene> s(new (std::nothrow) vrt_scene);
+        if (!s)
+                return fail(VRT_E_NOMEM, "scene alloc");
+        s->device = device;
+        s->max_depth = max_depth;
+        s->ntri = d->ntri;
+        const double t0 = now_ms();
+        try {
+                rc = build_tree(s.get(), d);
+                if (rc)
+                        return rc;
+                const int n = d->ntri;
+                s->tri_pos.resize((size_t)n);
+                s->tri_attr.resize((size_t)n);
+                for (int i = 0; i < n; ++i) {
+                        TriPos &tp = s->tri_pos[i];
+                        std::memcpy(tp.p, d->pos + 9 * (size_t)i, sizeof tp.p);
+                        tp.pad[0] = tp.pad[1] = tp.pad[2] = 0.f;
+                        TriAttr &ta = s->tri_attr[i];
+                        for (int v = 0; v < 3; ++v) {
+                                const float *nn = d->nrm + 9 * (size_t)i + 3 * v;
+                                const f3 q = normalize(mk3(nn[0], nn[1], nn[2]));
+                                ta.n[3 * v + 0] = q.x;
+                                ta.n[3 * v + 1] = q.y;
+                                ta.n[3 * v + 2] = q.z;
+                        }
+                        for (int k = 0; k < 6; ++k)
+                                ta.t[k] = d->uv ? d->uv[6 * (size_t)i + k] : 0.f;
+                        ta.mat = d->mat ? d->mat[i] : 0;
+                }
+                s->mats.resize((size_t)d->nmat);
+                for (int m = 0; m < d->nmat; ++m) {
+                        s->mats[m].tex = d->mat_tex[m];
+                        for (int k = 0; k < 3; ++k)
+                                s->mats[m].kd[k] = d->mat_kd[3 * m + k];
+                }
+                s->texs.resize((size_t)d->ntex);
+                for (int t = 0; t < d->ntex; ++t) {
+                        s->texs[t].off = d->tex_off[t];
+                        s->texs[t].w = d->tex_dims[3 * t];
+                        s->texs[t].h = d->tex_dims[3 * t + 1];
+                        s->texs[t].c = d->tex_dims[3 * t + 2];
+                        s->texs[t].pad = 0;
+                }
+                s->tex_bytes = d->ntex ? d->tex_bytes : 0;
+        } catch (const std::bad_alloc &) {
+                return fail(VRT_E_NOMEM, "octree build: out of host memory");
+        }
+        s->info.build_ms = now_ms() - t0;
+        s->info.max_depth = max_depth;
+        s->info.device = device;
+        const double t1 = now_ms();
+        if (device < 0) {  // host-only scene: build and inspect, no device
+                *out = s.release();
+                return VRT_OK;
+        }
+        rc = upload(s.get(), d);
+        if (rc) {
+                vrt_scene_destroy(s.release());
+                return rc;
+        }
+        s->info.upload_ms = now_ms() - t1;
+        *out = s.release();
+        return VRT_OK;
+}
+
+extern "C" void vrt_scene_destroy(vrt_scene *s)
+{
+        if (!s)
+                return;
+        if (s->d_mem || s->stream || s->ev0 || s->ev1) {
+                (void)hipSetDevice(s->device);
+                if (s->stream)
+                        (void)hipStreamSynchronize(s->stream);
+                if (s->d_mem)
+                        (void)hipFree(s->d_mem);
+                if (s->ev0)
+                        (void)hipEventDestroy(s->ev0);
+                if (s->ev1)
+                        (void)hipEventDestroy(s->ev1);
+                if (s->stream)
+                        (void)hipStreamDestroy(s->stream);
+        }
+        delete s;
+}
+
+extern "C" int vrt_scene_info(const vrt_scene *s, vrt_scene_info_t *info)
+{
+        if (!s || !info)
+                return fail(VRT_E_INVALID, "null argument");
+        *info = s->info;
+        return VRT_OK;
+}
+
+extern "C" int vrt_scene_leaves(const vrt_scene *s, uint32_t *voxel,
+                                uint32_t *count, int32_t *tris)
+{
+        if (!s || !voxel || !count || !tris)
+                return fail(VRT_E_INVALID, "null argument");
+        std::vector<std::pair<uint32_t, size_t>> lv;
+        for (size_t i = 0; i < s->nodes.size(); ++i) {
+                const NodeRec &nr = s->nodes[i];
+                if ((nr.a & kLeafBit) && (nr.a & ~kLeafBit))
+                        lv.emplace_back(s->node_vox[i], i);
+        }
+        std::sort(lv.begin(), lv.end());
+        size_t o = 0;
+        for (size_t j = 0; j < lv.size(); ++j) {
+                const NodeRec &nr = s->nodes[lv[j].second];
+                const uint32_t n = nr.a & ~kLeafBit;
+                voxel[j] = lv[j].first;
+                count[j] = n;
+                for (uint32_t k = 0; k < n; ++k)
+                        tris[o++] = (int32_t)s->refs[nr.b + k].tri;
+        }
+        return VRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// render
+// ---------------------------------------------------------------------------
+static int need_device(const vrt_scene *s)
+{
+        if (!s->d_mem)
+                return fail(VRT_E_NODEVICE, "scene was created host-only (device < 0)");
+        return VRT_OK;
+}
+
+static int film_ok(const vrt_film *f)
+{
+        if (!f || f->nx < 1 || f->ny < 1 || f->nx > 32768 || f->ny > 32768)
+                return fail(VRT_E_INVALID, "bad film");
+        return VRT_OK;
+}
+
+extern "C" int vrt_tiles_per_rank(const vrt_film *film, int nranks)
+{
+        if (film_ok(film) || nranks < 1)
+                return 0;
+        const int T = (film->nx / 8) * (film->ny / 8);
+        return (T + nranks - 1) / nranks;
+}
+
+static void fill_render_params(vrt_scene *s, const vrt_camera *cam,
+                               const vrt_film *film, int rank, int nranks,
+                               RenderParams *p)
+{
+        std::memset(p, 0, sizeof *p);
+        p->sc = s->dev;
+        fill_cam_params(cam, film, &p->cam);
+        p->ntx = film->nx / 8;
+        p->nty = film->ny / 8;
+        p->rank = rank;
+        p->nranks = nranks;
+        const int T = p->ntx * p->nty;
+        p->tiles_this_rank = rank < T ? (T - rank + nranks - 1) / nranks : 0;
+}
+
+extern "C" int vrt_render_tiles_device(vrt_scene *s, const vrt_camera *cam,
+                                       const vrt_film *film, int rank,
+                                       int nranks, int image_layout,
+                                       float *d_out, void *stream)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !cam || !d_out)
+                return fail(VRT_E_INVALID, "null argument");
+        if (int rc = film_ok(film))
+                return rc;
+        if (nranks < 1 || rank < 0 || rank >= nranks)
+                return fail(VRT_E_INVALID, "rank %d of %d", rank, nranks);
+        if (image_layout && nranks != 1)
+                return fail(VRT_E_INVALID, "image_layout requires nranks == 1");
+        HIPCHK(hipSetDevice(s->device));
+        RenderParams p;
+        fill_render_params(s, cam, film, rank, nranks, &p);
+        p.image_layout = image_layout;
+        p.out = d_out;
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        HIPCHK(hipEventRecord(s->ev0, st));
+        HIPCHK(launch_render(p, false, st));
+        HIPCHK(hipEventRecord(s->ev1, st));
+        s->timed = true;
+        return VRT_OK;
+}
+
+extern "C" int vrt_last_kernel_ms(vrt_scene *s, float *ms)
+{
+        if (!s || !ms)
+                return fail(VRT_E_INVALID, "null argument");
+        if (!s->timed)
+                return fail(VRT_E_INVALID, "no timed launch yet");
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipEventSynchronize(s->ev1));
+        HIPCHK(hipEventElapsedTime(ms, s->ev0, s->ev1));
+        return VRT_OK;
+}
+
+extern "C" int vrt_unpack_tiles_device(const vrt_film *film, int nranks,
+                                       const float *d_gathered, float *d_image,
+                                       void *stream)
+{
+        if (!d_gathered || !d_image || nranks < 1)
+                return fail(VRT_E_INVALID, "bad argument");
+        if (int rc = film_ok(film))
+                return rc;
+        const int tpr = vrt_tiles_per_rank(film, nranks);
+        HIPCHK(launch_unpack(film->nx, film->ny, film->nx / 8, film->ny / 8, nranks, tpr,
+                             d_gathered, d_image, static_cast<hipStream_t>(stream)));
+        return VRT_OK;
+}
+
+namespace {
+struct DevBuf {
+        void *p = nullptr;
+        ~DevBuf()
+        {
+                if (p)
+                        (void)hipFree(p);
+        }
+};
+}  // namespace
+
+extern "C" int vrt_render(vrt_scene *s, const vrt_camera *cam,
+                          const vrt_film *film, float *rgb,
+                          const vrt_samples *samples, vrt_stats *stats)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !cam || !rgb)
+                return fail(VRT_E_INVALID, "null argument");
+        if (int rc = film_ok(film))
+                return rc;
+        std::lock_guard<std::mutex> lk(s->mu);
+        HIPCHK(hipSetDevice(s->device));
+        const size_t npix = (size_t)film->nx * film->ny;
+        const size_t ns = npix * 4;
+        const bool want_cnt = (samples && samples->counters) || stats;
+        DevBuf img, shit, stri, svox, srgb, scnt;
+        HIPCHK(hipMalloc(&img.p, npix * 3 * sizeof(float)));
+        HIPCHK(hipMemsetAsync(img.p, 0, npix * 3 * sizeof(float), s->stream));
+        RenderParams p;
+        fill_render_params(s, cam, film, 0, 1, &p);
+        p.image_layout = 1;
+        p.out = static_cast<float *>(img.p);
+        auto alloc_fill = [&](DevBuf &b, size_t bytes, int byte) -> hipError_t {
+                hipError_t e = hipMalloc(&b.p, bytes);
+                if (e != hipSuccess)
+                        return e;
+                return hipMemsetAsync(b.p, byte, bytes, s->stream);
+        };
+        if (samples && samples->hit) {
+                HIPCHK(alloc_fill(shit, ns * 4, 0));
+                p.so.hit = static_cast<int32_t *>(shit.p);
+        }
+        if (samples && samples->tri) {
+                HIPCHK(alloc_fill(stri, ns * 4, 0xFF));
+                p.so.tri = static_cast<int32_t *>(stri.p);
+        }
+        if (samples && samples->voxel) {
+                HIPCHK(alloc_fill(svox, ns * 4, 0xFF));
+                p.so.vox = static_cast<uint32_t *>(svox.p);
+        }
+        if (samples && samples->rgb) {
+                HIPCHK(alloc_fill(srgb, ns * 12, 0));
+                p.so.rgb = static_cast<float *>(srgb.p);
+        }
+        if (want_cnt) {
+                HIPCHK(alloc_fill(scnt, ns * 16, 0));
+                p.so.cnt = static_cast<uint32_t *>(scnt.p);
+        }
+        HIPCHK(hipEventRecord(s->ev0, s->stream));
+        HIPCHK(launch_render(p, want_cnt, s->stream));
+        HIPCHK(hipEventRecord(s->ev1, s->stream));
+        s->timed = true;
+        HIPCHK(hipStreamSynchronize(s->stream));
+        HIPCHK(hipMemcpy(rgb, img.p, npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
+        if (p.so.hit)
+                HIPCHK(hipMemcpy(samples->hit, shit.p, ns * 4, hipMemcpyDeviceToHost));
+        if (p.so.tri)
+                HIPCHK(hipMemcpy(samples->tri, stri.p, ns * 4, hipMemcpyDeviceToHost));
+        if (p.so.vox)
+                HIPCHK(hipMemcpy(samples->voxel, svox.p, ns * 4, hipMemcpyDeviceToHost));
+        if (p.so.rgb)
+                HIPCHK(hipMemcpy(samples->rgb, srgb.p, ns * 12, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> cnt;
+        if (want_cnt) {
+                cnt.resize(ns * 4);
+                HIPCHK(hipMemcpy(cnt.data(), scnt.p, ns * 16, hipMemcpyDeviceToHost));
+                if (samples && samples->counters)
+                        std::memcpy(samples->counters, cnt.data(), ns * 16);
+        }
+        if (stats) {
+                std::memset(stats, 0, sizeof *stats);
+                const int W8 = 8 * (film->nx / 8), H8 = 8 * (film->ny / 8);
+                for (int py = 0; py < H8; ++py)
+                        for (int px = 0; px < W8; ++px)
+                                for (int q = 0; q < 4; ++q) {
+                                        const uint32_t *c = &cnt[(((size_t)py * film->nx + px) * 4 + q) * 4];
+                                        stats->rays++;
+                                        stats->aabb_tests += c[0];
+                                        stats->leaves += c[1];
+                                        stats->tri_tests += c[2];
+                                        stats->hits += c[3];
+                                }
+                float ms = 0.f;
+                HIPCHK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+                stats->kernel_ms = ms;
+        }
+        return VRT_OK;
+}
+
+extern "C" int vrt_ray_march_batch_device(vrt_scene *s, const vrt_ray *d_rays,
+                                          int64_t n, vrt_hit *d_hits,
+                                          void *stream)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || (n > 0 && (!d_rays || !d_hits)) || n < 0)
+                return fail(VRT_E_INVALID, "bad argument");
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(launch_ray_march(s->dev, d_rays, n, d_hits, static_cast<hipStream_t>(stream)));
+        return VRT_OK;
+}
+
+extern "C" int vrt_ray_march_batch(vrt_scene *s, const vrt_ray *rays,
+                                   int64_t n, vrt_hit *hits)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        static_assert(sizeof(vrt_ray) == 32, "vrt_ray layout");
+        static_assert(sizeof(vrt_hit) == 36, "vrt_hit layout");
+        if (!s || n < 0 || (n > 0 && (!rays || !hits)))
+                return fail(VRT_E_INVALID, "bad argument");
+        if (n == 0)
+                return VRT_OK;
+        std::lock_guard<std::mutex> lk(s->mu);
+        HIPCHK(hipSetDevice(s->device));
+        DevBuf dr, dh;
+        HIPCHK(hipMalloc(&dr.p, (size_t)n * sizeof(vrt_ray)));
+        HIPCHK(hipMalloc(&dh.p, (size_t)n * sizeof(vrt_hit)));
+        HIPCHK(hipMemcpy(dr.p, rays, (size_t)n * sizeof(vrt_ray), hipMemcpyHostToDevice));
+        HIPCHK(launch_ray_march(s->dev, dr.p, n, dh.p, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        HIPCHK(hipMemcpy(hits, dh.p, (size_t)n * sizeof(vrt_hit), hipMemcpyDeviceToHost));
+        return VRT_OK;
+}
+
+extern "C" int vrt_device_selftest(int device, const double *mt_in,
+                                   double *mt_out, const float *sat_in,
+                                   int32_t *sat_out, int64_t n)
+{
+        if (n < 0 || (mt_in && !mt_out) || (sat_in && !sat_out))
+                return fail(VRT_E_INVALID, "bad argument");
+        if (int rc = check_device(device))
+                return rc;
+        HIPCHK(hipSetDevice(device));
+        DevBuf a, b, c, d;
+        if (mt_in) {
+                HIPCHK(hipMalloc(&a.p, (size_t)n * 15 * 8));
+                HIPCHK(hipMalloc(&b.p, (size_t)n * 4 * 8));
+                HIPCHK(hipMemcpy(a.p, mt_in, (size_t)n * 15 * 8, hipMemcpyHostToDevice));
+        }
+        if (sat_in) {
+                HIPCHK(hipMalloc(&c.p, (size_t)n * 15 * 4));
+                HIPCHK(hipMalloc(&d.p, (size_t)n * 4));
+                HIPCHK(hipMemcpy(c.p, sat_in, (size_t)n * 15 * 4, hipMemcpyHostToDevice));
+        }
+        HIPCHK(launch_selftest(static_cast<double *>(a.p), static_cast<double *>(b.p),
+                               static_cast<float *>(c.p), static_cast<int32_t *>(d.p), n, nullptr));
+        HIPCHK(hipDeviceSynchronize());
+        if (mt_in)
+                HIPCHK(hipMemcpy(mt_out, b.p, (size_t)n * 4 * 8, hipMemcpyDeviceToHost));
+        if (sat_in)
+                HIPCHK(hipMemcpy(sat_out, d.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+        return VRT_OK;
+}

@@ -1,0 +1,114 @@
+// vrt_internal.h -- device data layout shared by the host library and the
+// gfx950 kernels.  See DESIGN.md "Data layout in HBM".
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "vrt_math.h"
+
+namespace vrt {
+
+// One octree node, 32 B (two dwordx4 loads).  The 8 children of an internal
+// node are contiguous.  Boxes are the exact float boxes split() produces
+// (VRT/voxel_octree.cc:27-39).
+//   internal:        a = index of first child      (bit 31 clear)
+//   leaf:            a = kLeafBit | triangle count, b = first ref record
+struct alignas(16) NodeRec {
+        float bmin[3];
+        float bmax[3];
+        uint32_t a;
+        uint32_t b;
+};
+static_assert(sizeof(NodeRec) == 32, "NodeRec must be 32 B");
+constexpr uint32_t kLeafBit = 0x80000000u;
+
+// One leaf-list entry with the triangle's vertices inlined (48 B, three
+// dwordx4): leaf lists are walked without a dependent index load.
+struct alignas(16) RefRec {
+        float p[9];
+        uint32_t tri;
+        uint32_t pad[2];
+};
+static_assert(sizeof(RefRec) == 48, "RefRec must be 48 B");
+
+// Shading attributes of one triangle (64 B): normalised vertex normals
+// (Triangle::Triangle, VRT/voxel_octree.cc:426), uvs, material id.
+struct alignas(16) TriAttr {
+        float n[9];
+        float t[6];
+        int32_t mat;
+};
+static_assert(sizeof(TriAttr) == 64, "TriAttr must be 64 B");
+
+struct alignas(16) TriPos {
+        float p[9];
+        float pad[3];
+};
+
+struct alignas(16) MatRec {
+        int32_t tex;  // -1 = untextured: Kd
+        float kd[3];
+};
+
+struct alignas(16) TexRec {
+        int64_t off;
+        int32_t w, h, c, pad;
+};
+
+// Device-side scene view passed by value to kernels.
+struct DevScene {
+        const NodeRec *nodes;
+        const uint32_t *node_vox;
+        const RefRec *refs;
+        const TriPos *tri_pos;
+        const TriAttr *tri_attr;
+        const MatRec *mats;
+        const TexRec *texs;
+        const uint8_t *tex_data;
+        int32_t max_depth;
+        int32_t nmat, ntex;
+};
+
+// Camera + film constants for ray generation (T1), computed on the host.
+struct CamParams {
+        float s[3], u[3], nf[3], e[3];  // columns of C_
+        float origin[3];                // point_transform(C_, {})
+        float z;                        // -(film.h / (2*tanf(fov/2)))
+        float tmin, tmax;               // near, far
+        int32_t nx, ny;
+};
+
+// Per-sample outputs (device pointers, any may be null).
+struct SampleOut {
+        int32_t *hit;
+        int32_t *tri;
+        uint32_t *vox;
+        float *rgb;
+        uint32_t *cnt;
+};
+
+struct RenderParams {
+        DevScene sc;
+        CamParams cam;
+        int32_t ntx, nty;      // 8x8 tiles in the render area
+        int32_t rank, nranks;  // tile t handled by rank t % nranks
+        int32_t tiles_this_rank;
+        int32_t image_layout;  // 1: out is nx*ny*3 image; 0: packed tiles
+        float *out;
+        SampleOut so;
+};
+
+// Kernel launchers (vrt_kernels.hip)
+hipError_t launch_render(const RenderParams &p, bool instrumented,
+                         hipStream_t st);
+hipError_t launch_ray_march(const DevScene &sc, const void *d_rays,
+                            int64_t n, void *d_hits, hipStream_t st);
+hipError_t launch_unpack(int nx, int ny, int ntx, int nty, int nranks,
+                         int tiles_per_rank, const float *src, float *dst,
+                         hipStream_t st);
+hipError_t launch_selftest(const double *mt_in, double *mt_out,
+                           const float *sat_in, int32_t *sat_out, int64_t n,
+                           hipStream_t st);
+
+}  // namespace vrt

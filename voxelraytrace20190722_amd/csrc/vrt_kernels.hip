@@ -1,0 +1,558 @@
+// vrt_kernels.hip -- gfx950 (CDNA4, wave64) kernels of the primary-ray hot
+// path: fused camera ray generation (T1), octree ray march (T2-T6), primary
+// shading (T7) and Film accumulation (T8) -- SURVEY §8(a).
+//
+// One ray per lane.  A 256-thread workgroup owns one 8x8-pixel screen tile;
+// each wave covers a 4x4-pixel quadrant x the 4 gen_rays4 samples (lane =
+// pixel*4 + sample), so the four samples of a pixel sit in adjacent lanes
+// and are summed in the reference's order with cross-lane reads.
+//
+// Traversal keeps the reference's result exactly (first DFS leaf with any
+// hit; nearest of that leaf's triangles), but restructures the work:
+//  * a node's 8 child boxes are never loaded: split() makes them from the
+//    parent box with exact float ops (VRT/voxel_octree.cc:27-39), so one
+//    32-B node record gives all 8 slab tests from 9 plane distances;
+//  * every child is slab-tested when its parent is expanded (the reference
+//    tests it when popped -- same outcome), and only the hit children are
+//    kept, ordered by the (dist, child index) key that libstdc++'s stable
+//    insertion sort produces (VRT/voxel_octree.cc:77-97), packed 3 bits
+//    each into one 24-bit word;
+//  * the DFS stack lives in LDS, [level][lane], 8 B per entry.
+//
+// VRT/x = /root/reference/VoxelRayTrace20190722/x
+#include "vrt_internal.h"
+
+namespace vrt {
+
+constexpr int kBlock = 256;
+constexpr int kStack = 12;  // >= VRT_MAX_DEPTH - 1 internal levels
+
+struct RayK {
+        f3 o, d, dinv;
+        float tmin, tmax;
+};
+
+__device__ __forceinline__ void load_node(const NodeRec *__restrict__ nodes,
+                                          uint32_t i, float bmin[3],
+                                          float bmax[3], uint32_t &a,
+                                          uint32_t &b)
+{
+        const float4 *q = reinterpret_cast<const float4 *>(nodes + i);
+        const float4 q0 = q[0];
+        const float4 q1 = q[1];
+        bmin[0] = q0.x; bmin[1] = q0.y; bmin[2] = q0.z;
+        bmax[0] = q0.w; bmax[1] = q1.x; bmax[2] = q1.y;
+        a = __float_as_uint(q1.z);
+        b = __float_as_uint(q1.w);
+}
+
+// Expand an internal node with box [bmin,bmax]: slab-test its 8 children
+// (boxes from split()'s exact arithmetic) and return the hit children in
+// travorder order, 3 bits each (first child in bits 0-2); cnt = number.
+// full_pos (instrumented only): 3-bit position of each child ci (bits 3ci)
+// in the full 8-child travorder order, for the reference's test counts.
+template <bool kFullPos>
+__device__ __forceinline__ uint32_t expand(const float bmin[3],
+                                           const float bmax[3],
+                                           const RayK &r, int &cnt,
+                                           uint32_t &full_pos)
+{
+        const float oo[3] = { r.o.x, r.o.y, r.o.z };
+        const float dd[3] = { r.d.x, r.d.y, r.d.z };
+        const float di[3] = { r.dinv.x, r.dinv.y, r.dinv.z };
+        float nr[3][2], fr[3][2], q[3][2];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+                // split(): half = size()/2; child.min = min + mask*half;
+                // child.max = child.min + half
+                const float h = (bmax[k] - bmin[k]) / 2.0f;
+                const float a0 = bmin[k] + 0.0f * h;  // mask 0 min
+                const float b = bmin[k] + h;          // mask 0 max == mask 1 min
+                const float a1 = a0 + h;              // mask 0 max (same op as b)
+                const float c = b + h;                // mask 1 max
+                // AABB3D::isect: (min - o) * dinv, (max - o) * dinv
+                const float ta = (a0 - oo[k]) * di[k];
+                const float tb0 = (a1 - oo[k]) * di[k];
+                const float tb1 = (b - oo[k]) * di[k];
+                const float tc = (c - oo[k]) * di[k];
+                nr[k][0] = std_min(ta, tb0);
+                fr[k][0] = std_max(ta, tb0);
+                nr[k][1] = std_min(tb1, tc);
+                fr[k][1] = std_max(tb1, tc);
+                // travorder: dot(d, center - o), center = (min + max) * .5f
+                q[k][0] = dd[k] * ((a0 + a1) * .5f - oo[k]);
+                q[k][1] = dd[k] * ((b + c) * .5f - oo[k]);
+        }
+        float dist[8];
+        uint32_t hm = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+                const int mx = (i >> 2) & 1, my = (i >> 1) & 1, mz = i & 1;
+                float t0 = nr[0][mx], t1 = fr[0][mx];
+                if (t0 < nr[1][my]) t0 = nr[1][my];  // max_element
+                if (t0 < nr[2][mz]) t0 = nr[2][mz];
+                if (fr[1][my] < t1) t1 = fr[1][my];  // min_element
+                if (fr[2][mz] < t1) t1 = fr[2][mz];
+                hm |= (slab_hit(t0, t1, r.tmin, r.tmax) ? 1u : 0u) << i;
+                dist[i] = (0.0f + q[0][mx] + q[1][my]) + q[2][mz];
+        }
+        // Stable order: j precedes i  <=>  !(dist_i < dist_j) for j < i.
+        uint32_t bef[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+                bef[i] = 0;
+#pragma unroll
+        for (int i = 1; i < 8; ++i) {
+#pragma unroll
+                for (int j = 0; j < i; ++j) {
+                        const bool c = dist[i] < dist[j];
+                        bef[i] |= (c ? 0u : 1u) << j;
+                        bef[j] |= (c ? 1u : 0u) << i;
+                }
+        }
+        uint32_t order = 0;
+        full_pos = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+                const uint32_t pos = __popc(bef[i] & hm);
+                order |= ((hm >> i) & 1u) ? ((uint32_t)i << (3 * pos)) : 0u;
+                if (kFullPos)
+                        full_pos |= (uint32_t)__popc(bef[i]) << (3 * i);
+        }
+        cnt = __popc(hm);
+        return order;
+}
+
+struct MarchResult {
+        bool hit;
+        uint32_t node;  // hit leaf
+        uint32_t tri;
+        float u, v;     // clamped barycentrics of the best triangle
+        f3 hp;          // ISect::hit
+        uint32_t A, L, T;  // reference-equivalent counters (instrumented)
+};
+
+// ray_march_isect (VRT/voxel_octree.cc:99-129) over one leaf's records.
+template <bool kCount>
+__device__ __forceinline__ bool leaf_isect(const RefRec *__restrict__ refs,
+                                           uint32_t first, uint32_t n,
+                                           const RayK &r, MarchResult &m)
+{
+        const double od[3] = { (double)r.o.x, (double)r.o.y, (double)r.o.z };
+        const double dv[3] = { (double)r.d.x, (double)r.d.y, (double)r.d.z };
+        bool any = false;
+        float best = 0.f;
+        for (uint32_t k = 0; k < n; ++k) {
+                const float4 *q = reinterpret_cast<const float4 *>(refs + first + k);
+                const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+                const double p0[3] = { q0.x, q0.y, q0.z };
+                const double p1[3] = { q0.w, q1.x, q1.y };
+                const double p2[3] = { q1.z, q1.w, q2.x };
+                double t, u, v;
+                if (mt_isect(od, dv, p0, p1, p2, &t, &u, &v)) {
+                        // Triangle::isect (VRT/voxel_octree.cc:449-454)
+                        const float fu = clampf((float)u, 0, 1);
+                        const float fv = clampf((float)v, 0, 1);
+                        const f3 hp = r.o + r.d * (float)t;
+                        const float depth = length(hp - r.o);
+                        // min_element: first strict minimum
+                        if (!any || depth < best) {
+                                any = true;
+                                best = depth;
+                                m.tri = __float_as_uint(q2.y);
+                                m.u = fu;
+                                m.v = fv;
+                                m.hp = hp;
+                        }
+                }
+        }
+        if (kCount)
+                m.T += n;
+        return any;
+}
+
+// gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
+// stack columns (stride kBlock).
+template <bool kCount>
+__device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
+                                          uint32_t *stk_base,
+                                          uint32_t *stk_ord,
+                                          uint32_t *stk_aux,
+                                          uint32_t *path_rem,
+                                          MarchResult &m)
+{
+        m.hit = false;
+        m.A = 1;
+        m.L = 0;
+        m.T = 0;
+        float bmin[3], bmax[3];
+        uint32_t a, b;
+        load_node(sc.nodes, 0, bmin, bmax, a, b);
+        if (!aabb_isect(bmin, bmax, r.o, r.dinv, r.tmin, r.tmax))
+                return;
+        if (a & kLeafBit) {
+                if (kCount)
+                        m.L++;
+                if (leaf_isect<kCount>(sc.refs, b, a & ~kLeafBit, r, m)) {
+                        m.hit = true;
+                        m.node = 0;
+                }
+                return;
+        }
+        int cnt;
+        uint32_t fpos;
+        uint32_t order = expand<kCount>(bmin, bmax, r, cnt, fpos);
+        uint32_t base = a;
+        uint32_t depth = 1;  // depth of the node whose children we walk
+        uint32_t nexp = 1;
+        int sp = 0;
+        for (;;) {
+                if (cnt == 0) {
+                        if (sp == 0)
+                                break;
+                        --sp;
+                        base = stk_base[sp * kBlock];
+                        const uint32_t w = stk_ord[sp * kBlock];
+                        order = w & 0xFFFFFFu;
+                        cnt = (int)(w >> 24);
+                        if (kCount) {
+                                const uint32_t x = stk_aux[sp * kBlock];
+                                fpos = x & 0xFFFFFFu;
+                                depth = x >> 24;
+                        }
+                        continue;
+                }
+                const uint32_t ci = order & 7u;
+                order >>= 3;
+                --cnt;
+                const uint32_t node = base + ci;
+                if (kCount)
+                        path_rem[depth * kBlock] = 7u - ((fpos >> (3 * ci)) & 7u);
+                load_node(sc.nodes, node, bmin, bmax, a, b);
+                if (!(a & kLeafBit)) {
+                        if (cnt) {
+                                stk_base[sp * kBlock] = base;
+                                stk_ord[sp * kBlock] = order | ((uint32_t)cnt << 24);
+                                if (kCount)
+                                        stk_aux[sp * kBlock] = fpos | (depth << 24);
+                                ++sp;
+                        }
+                        order = expand<kCount>(bmin, bmax, r, cnt, fpos);
+                        base = a;
+                        ++depth;
+                        ++nexp;
+                        continue;
+                }
+                if (kCount)
+                        m.L++;
+                const uint32_t n = a & ~kLeafBit;
+                if (n && leaf_isect<kCount>(sc.refs, b, n, r, m)) {
+                        m.hit = true;
+                        m.node = node;
+                        break;
+                }
+        }
+        if (kCount) {
+                // 1 root test + 8 per expanded node, minus the children the
+                // reference never popped on the path it stopped on.
+                uint32_t A = 1 + 8 * nexp;
+                if (m.hit)
+                        for (uint32_t lv = 1; lv <= depth; ++lv)
+                                A -= path_rem[lv * kBlock];
+                m.A = A;
+        }
+}
+
+__device__ __forceinline__ RayK make_rayk(f3 o, f3 dn, float tmin, float tmax)
+{
+        RayK r;
+        r.o = o;
+        r.d = dn;
+        r.dinv = mk3(dinv_of(dn.x), dinv_of(dn.y), dinv_of(dn.z));
+        r.tmin = tmin;
+        r.tmax = tmax;
+        return r;
+}
+
+// Triangle::get_diffuse(isect, ray, (1,1,1)) (VRT/voxel_octree.cc:462-484)
+// with Triangle::isect's normal (VRT/voxel_octree.cc:451-453).
+__device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
+                                        const MarchResult &m, f3 &normal)
+{
+        const TriAttr *ta = sc.tri_attr + m.tri;
+        const float4 *q = reinterpret_cast<const float4 *>(ta);
+        const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+        const f3 n0 = mk3(a0.x, a0.y, a0.z), n1 = mk3(a0.w, a1.x, a1.y),
+                 n2 = mk3(a1.z, a1.w, a2.x);
+        const float t0u = a2.y, t0v = a2.z, t1u = a2.w, t1v = a3.x,
+                    t2u = a3.y, t2v = a3.z;
+        const int mat = __float_as_int(a3.w);
+        const float w = clampf(1.0f - m.u - m.v, 0, 1);
+        normal = normalize((n0 * w + n1 * m.u) + n2 * m.v);
+        const MatRec mr = sc.mats[mat];
+        f3 albedo;
+        if (mr.tex < 0) {
+                albedo = mk3(mr.kd[0], mr.kd[1], mr.kd[2]);
+        } else {
+                const float4 *pp = reinterpret_cast<const float4 *>(sc.tri_pos + m.tri);
+                const float4 p0 = pp[0], p1 = pp[1], p2 = pp[2];
+                f3 bc = barycentric(m.hp, mk3(p0.x, p0.y, p0.z),
+                                    mk3(p0.w, p1.x, p1.y),
+                                    mk3(p1.z, p1.w, p2.x));
+                bc.x = clampf(bc.x, 0.f, 1.f);
+                bc.y = clampf(bc.y, 0.f, 1.f);
+                bc.z = clampf(bc.z, 0.f, 1.f);
+                const float tu = (bc.x * t0u + bc.y * t1u) + bc.z * t2u;
+                const float tv = (bc.x * t0v + bc.y * t1v) + bc.z * t2v;
+                const TexRec tx = sc.texs[mr.tex];
+                const int x = clampi((int)(unit_cycle(tu) * (float)tx.w), 0, tx.w - 1);
+                int y = clampi((int)(unit_cycle(tv) * (float)tx.h), 0, tx.h - 1);
+                y = tx.h - 1 - y;
+                const uint8_t *p = sc.tex_data + tx.off +
+                                   ((int64_t)y * tx.w + x) * tx.c;
+                const float c0 = (float)p[0];
+                const float c1 = tx.c > 1 ? (float)p[1] : 0.f;
+                const float c2 = tx.c > 2 ? (float)p[2] : 0.f;
+                albedo = mk3(c0 / 255.f, c1 / 255.f, c2 / 255.f);
+        }
+        float tmp = dot(normal, -r.d);
+        tmp = clampf(tmp, 0.f, 1.f);
+        const f3 c = albedo * tmp;
+        return mk3(c.x * 1.0f, c.y * 1.0f, c.z * 1.0f);  // * color (1,1,1)
+}
+
+// ---------------------------------------------------------------------------
+// Primary render: one workgroup per 8x8 tile.
+// ---------------------------------------------------------------------------
+template <bool kCount>
+__global__ __launch_bounds__(kBlock) void k_render(RenderParams p)
+{
+        __shared__ uint32_t stk_base[kStack * kBlock];
+        __shared__ uint32_t stk_ord[kStack * kBlock];
+        __shared__ uint32_t stk_aux[kCount ? kStack * kBlock : 1];
+        __shared__ uint32_t path_rem[kCount ? (kStack + 1) * kBlock : 1];
+
+        const int tid = threadIdx.x;
+        // XCD-aware tile order: blocks b, b+8, ... run on one XCD; give them
+        // consecutive tiles so each XCD's L2 serves one screen region.
+        const int nb = gridDim.x;
+        const int b = blockIdx.x;
+        const int per = (nb + 7) >> 3;
+        const int xcd = b & 7, slot = b >> 3;
+        int k = xcd * per + slot;
+        if ((nb & 7) != 0) {
+                // uneven grid: fall back to the identity map
+                k = b;
+        }
+        if (k >= p.tiles_this_rank)
+                return;
+        const int t = p.rank + k * p.nranks;
+        const int tx = t % p.ntx, ty = t / p.ntx;
+        const int wave = tid >> 6, lane = tid & 63;
+        const int s = lane & 3, pix = lane >> 2;
+        const int lx = (wave & 1) * 4 + (pix & 3);
+        const int ly = (wave >> 1) * 4 + (pix >> 2);
+        const int px = tx * 8 + lx, py = ty * 8 + ly;
+        const CamParams &c = p.cam;
+
+        // Camera::gen_rays4 (VRT/camera.cc:95-112)
+        const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
+                                 sample_x(s), sample_y(s));
+        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
+                                 dn, c.tmin, c.tmax);
+
+        MarchResult m;
+        ray_march<kCount>(p.sc, r, stk_base + tid, stk_ord + tid,
+                          stk_aux + (kCount ? tid : 0),
+                          path_rem + (kCount ? tid : 0), m);
+
+        f3 col;
+        if (m.hit) {
+                f3 nrm;
+                col = shade_hit(p.sc, r, m, nrm);
+        } else {
+                col = sky(r.d.y);
+        }
+
+        const size_t si = ((size_t)py * c.nx + px) * 4 + s;
+        if (p.so.hit) p.so.hit[si] = m.hit ? 1 : 0;
+        if (p.so.tri) p.so.tri[si] = m.hit ? (int32_t)m.tri : -1;
+        if (p.so.vox) p.so.vox[si] = m.hit ? p.sc.node_vox[m.node] : 0xFFFFFFFFu;
+        if (p.so.rgb) {
+                p.so.rgb[3 * si + 0] = col.x;
+                p.so.rgb[3 * si + 1] = col.y;
+                p.so.rgb[3 * si + 2] = col.z;
+        }
+        if (kCount && p.so.cnt) {
+                p.so.cnt[4 * si + 0] = m.A;
+                p.so.cnt[4 * si + 1] = m.L;
+                p.so.cnt[4 * si + 2] = m.T;
+                p.so.cnt[4 * si + 3] = m.hit ? 1u : 0u;
+        }
+
+        // Film::add(px, py, c * .25f) for samples 0..3 in order, starting
+        // from the zero-initialised film (VRT/camera.cc:17-20, main.cc:121).
+        const f3 cq = col * .25f;
+        const int l0 = lane & ~3;
+        float acc[3] = { 0.0f, 0.0f, 0.0f };
+        const float cv[3] = { cq.x, cq.y, cq.z };
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                        acc[q] += __shfl(cv[q], l0 + j, 64);
+        }
+        if (s == 0) {
+                float *o;
+                if (p.image_layout)
+                        o = p.out + ((size_t)py * c.nx + px) * 3;
+                else
+                        o = p.out + ((size_t)k * 64 + ly * 8 + lx) * 3;
+                o[0] = acc[0];
+                o[1] = acc[1];
+                o[2] = acc[2];
+        }
+}
+
+// ---------------------------------------------------------------------------
+// Batched gi::ray_march over arbitrary rays: one ray per lane.
+// Output record = vrt_hit {hit, tri, voxel, hit_p[3], normal[3]} (36 B).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_ray_march(DevScene sc,
+                                                      const float *__restrict__ rays,
+                                                      int64_t n,
+                                                      uint32_t *__restrict__ out)
+{
+        __shared__ uint32_t stk_base[kStack * kBlock];
+        __shared__ uint32_t stk_ord[kStack * kBlock];
+        const int tid = threadIdx.x;
+        const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
+        if (i >= n)
+                return;
+        const float *rr = rays + 8 * i;
+        const RayK r = make_rayk(mk3(rr[0], rr[1], rr[2]), mk3(rr[3], rr[4], rr[5]),
+                                 rr[6], rr[7]);
+        MarchResult m;
+        ray_march<false>(sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        uint32_t *o = out + 9 * i;
+        if (m.hit) {
+                f3 nrm;
+                const TriAttr *ta = sc.tri_attr + m.tri;
+                const f3 n0 = mk3(ta->n[0], ta->n[1], ta->n[2]);
+                const f3 n1 = mk3(ta->n[3], ta->n[4], ta->n[5]);
+                const f3 n2 = mk3(ta->n[6], ta->n[7], ta->n[8]);
+                const float w = clampf(1.0f - m.u - m.v, 0, 1);
+                nrm = normalize((n0 * w + n1 * m.u) + n2 * m.v);
+                o[0] = 1;
+                o[1] = m.tri;
+                o[2] = sc.node_vox[m.node];
+                o[3] = __float_as_uint(m.hp.x);
+                o[4] = __float_as_uint(m.hp.y);
+                o[5] = __float_as_uint(m.hp.z);
+                o[6] = __float_as_uint(nrm.x);
+                o[7] = __float_as_uint(nrm.y);
+                o[8] = __float_as_uint(nrm.z);
+        } else {
+                o[0] = 0;
+                o[1] = 0xFFFFFFFFu;
+                o[2] = 0xFFFFFFFFu;
+                for (int q = 3; q < 9; ++q)
+                        o[q] = 0;
+        }
+}
+
+// Rank-0 re-assembly of gathered per-rank tile buffers into the image.
+__global__ void k_unpack(int nx, int ny, int ntx, int nty, int nranks,
+                         int tpr, const float *__restrict__ src,
+                         float *__restrict__ dst)
+{
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= (int64_t)nx * ny)
+                return;
+        const int px = (int)(i % nx), py = (int)(i / nx);
+        const int tx = px >> 3, ty = py >> 3;
+        float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+        if (tx < ntx && ty < nty) {
+                const int t = ty * ntx + tx;
+                const int r = t % nranks, k = t / nranks;
+                const float *q = src + (((int64_t)r * tpr + k) * 64 + (py & 7) * 8 + (px & 7)) * 3;
+                v0 = q[0];
+                v1 = q[1];
+                v2 = q[2];
+        }
+        dst[3 * i + 0] = v0;
+        dst[3 * i + 1] = v1;
+        dst[3 * i + 2] = v2;
+}
+
+// Device copies of the MT / SAT leaves for bit-exact KATs.
+__global__ void k_selftest(const double *mt_in, double *mt_out,
+                           const float *sat_in, int32_t *sat_out, int64_t n)
+{
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= n)
+                return;
+        if (mt_in) {
+                const double *q = mt_in + 15 * i;
+                double t = 0, u = 0, v = 0;
+                const int ret = mt_isect(q, q + 3, q + 6, q + 9, q + 12, &t, &u, &v);
+                mt_out[4 * i + 0] = ret;
+                mt_out[4 * i + 1] = ret ? t : 0.0;
+                mt_out[4 * i + 2] = ret ? u : 0.0;
+                mt_out[4 * i + 3] = ret ? v : 0.0;
+        }
+        if (sat_in) {
+                const float *q = sat_in + 15 * i;
+                sat_out[i] = tri_box_overlap(q, q + 3, q + 6);
+        }
+}
+
+hipError_t launch_render(const RenderParams &p, bool instrumented,
+                         hipStream_t st)
+{
+        if (p.tiles_this_rank <= 0)
+                return hipSuccess;
+        // round the grid up to a multiple of 8 (one slot per XCD)
+        const int grid = (p.tiles_this_rank + 7) & ~7;
+        if (instrumented)
+                hipLaunchKernelGGL(k_render<true>, dim3(grid), dim3(kBlock), 0, st, p);
+        else
+                hipLaunchKernelGGL(k_render<false>, dim3(grid), dim3(kBlock), 0, st, p);
+        return hipGetLastError();
+}
+
+hipError_t launch_ray_march(const DevScene &sc, const void *d_rays, int64_t n,
+                            void *d_hits, hipStream_t st)
+{
+        if (n <= 0)
+                return hipSuccess;
+        const int64_t grid = (n + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(k_ray_march, dim3((unsigned)grid), dim3(kBlock), 0, st,
+                           sc, static_cast<const float *>(d_rays), n,
+                           static_cast<uint32_t *>(d_hits));
+        return hipGetLastError();
+}
+
+hipError_t launch_unpack(int nx, int ny, int ntx, int nty, int nranks,
+                         int tpr, const float *src, float *dst, hipStream_t st)
+{
+        const int64_t n = (int64_t)nx * ny;
+        if (n <= 0)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_unpack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                           nx, ny, ntx, nty, nranks, tpr, src, dst);
+        return hipGetLastError();
+}
+
+hipError_t launch_selftest(const double *mt_in, double *mt_out,
+                           const float *sat_in, int32_t *sat_out, int64_t n,
+                           hipStream_t st)
+{
+        if (n <= 0)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_selftest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                           mt_in, mt_out, sat_in, sat_out, n);
+        return hipGetLastError();
+}
+
+}  // namespace vrt
