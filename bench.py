@@ -51,6 +51,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-counters", action="store_true")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl (RCCL over xGMI, the real path) or gloo (host-staged rehearsal)")
+    p.add_argument("--save-image", default="", help="rank 0 writes the last frame as .hdr")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
@@ -62,10 +65,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus={a.gpus}; using WORLD_SIZE")
+    local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     # ---- scene: built on the host, uploaded once (excluded from timing)
     t0 = time.time()
@@ -90,11 +97,24 @@ def main():
     tpr = vrt.tiles_per_rank(film, world)
     img = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev)
     if world > 1:
-        tiles = torch.zeros(tpr * 192, dtype=torch.float32, device=dev)
-        gl = [torch.zeros_like(tiles) for _ in range(world)] if rank == 0 else None
-        gathered = torch.zeros((world, tpr * 192), dtype=torch.float32, device=dev) if rank == 0 else None
+        # double-buffered: the RCCL gather of frame k (on the NCCL stream)
+        # overlaps the render of frame k+1 (on the compute stream)
+        tiles = [torch.zeros(tpr * 192, dtype=torch.float32, device=dev) for _ in range(2)]
+        gathered = ([torch.zeros((world, tpr * 192), dtype=torch.float32, device=dev) for _ in range(2)]
+                    if rank == 0 else None)
+        gl = [list(g.unbind(0)) for g in gathered] if rank == 0 else [None, None]  # in-place views
+    works = [None, None]
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(a.steps)]
+
+    def finish(b):
+        """Rank 0: re-assemble the frame gathered into buffer b."""
+        if works[b] is None:
+            return
+        works[b].wait()  # stream-wait on the gather, no host block
+        works[b] = None
+        if rank == 0:
+            vrt.unpack_tiles_device(film, world, gathered[b].data_ptr(), img.data_ptr(), sp)
 
     def step(k, timed):
         cam = cams[k % a.poses]
@@ -105,16 +125,29 @@ def main():
             if timed:
                 ev[k][1].record(stream)
             return
-        tree.render_tiles_device(cam, film, rank, world, 0, tiles.data_ptr(), sp)
+        b = k & 1
+        finish(b)  # frame k-2 used this buffer pair
+        tree.render_tiles_device(cam, film, rank, world, 0, tiles[b].data_ptr(), sp)
         if timed:
             ev[k][1].record(stream)
-        dist.gather(tiles, gl, dst=0)
-        if rank == 0:
-            torch.stack(gl, out=gathered)
-            vrt.unpack_tiles_device(film, world, gathered.data_ptr(), img.data_ptr(), sp)
+        finish(1 - b)  # frame k-1: its gather overlapped this render
+        if a.dist_backend == "nccl":
+            works[b] = dist.gather(tiles[b], gl[b], dst=0, async_op=True)
+        else:  # gloo rehearsal (several ranks on one GPU): host-staged gather
+            host = tiles[b].cpu()
+            hl = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+            dist.gather(host, hl, dst=0)
+            if rank == 0:
+                gathered[b].copy_(torch.stack(hl))
+                vrt.unpack_tiles_device(film, world, gathered[b].data_ptr(), img.data_ptr(), sp)
+
+    def drain():
+        finish(0)
+        finish(1)
 
     for k in range(a.warmup):
         step(k, False)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -122,13 +155,14 @@ def main():
     t_start = time.perf_counter()
     for k in range(a.steps):
         step(k, True)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kms = np.array([s.elapsed_time(e) for s, e in ev])  # render kernel, ms
@@ -181,21 +215,24 @@ def main():
         fov, eye, spot, up = vrt.sweep_pose(mn, mx, 0, a.poses)
         oc = po.camera(fov, eye, spot, up)
         nth = max(1, min(a.cpu_threads, os.cpu_count() or 1))
-        stride = 64
-        sec, _ = osc.render_rows(oc, 1.0, 1.0, a.width, a.height, stride, 0, nth)
-        rows = len(range(0, H8, stride))
-        rate = rows * W8 * 4 / max(sec, 1e-6)
-        want_rows = max(1, int(rate * a.cpu_seconds / (W8 * 4)))
-        stride = max(1, H8 // want_rows)
-        sec, _ = osc.render_rows(oc, 1.0, 1.0, a.width, a.height, stride, 0, nth)
-        rows = len(range(0, H8, stride))
-        cpu_rays = rows * W8 * 4
+        # bounded sample: whole frames of the sweep (poses 0,1,..) until the
+        # target CPU time is spent, at least one frame
+        cpu_rays, sec, frames = 0, 0.0, 0
+        while frames == 0 or (sec < a.cpu_seconds and frames < a.poses):
+            fov, eye, spot, up = vrt.sweep_pose(mn, mx, frames % a.poses, a.poses)
+            oc = po.camera(fov, eye, spot, up)
+            s_, _ = osc.render_rows(oc, 1.0, 1.0, a.width, a.height, 1, 0, nth)
+            sec += s_
+            cpu_rays += rays_per_frame
+            frames += 1
         cpu = {"value": round(cpu_rays / sec / 1e6, 4), "unit": "Mrays/s", "cores": nth, "kind": "port",
-               "sample": f"every {stride}th row ({rows} rows x {W8} px x 4 spp = {cpu_rays} rays) of the "
-                         f"{a.width}x{a.height} frame at sweep pose 0, {sec:.1f} s, oracle/vrt_oracle.c "
-                         f"over {nth} threads"}
+               "sample": f"{frames} full {a.width}x{a.height} x4 spp frames (sweep poses 0..{frames - 1}, "
+                         f"{cpu_rays} rays, {sec:.1f} s) rendered by oracle/vrt_oracle.c with render_mt's "
+                         f"8x8 tiles over {nth} threads"}
         osc.close()
 
+    if rank == 0 and a.save_image:
+        vrt.write_hdr(a.save_image, img.cpu().numpy())
     if rank == 0:
         total_rays = rays_per_frame * a.steps
         value = total_rays / elapsed / 1e6
@@ -209,7 +246,8 @@ def main():
                                    f"({sd.ntri} tris), max_depth {a.depth} (\"256^3\")",
                        "width": a.width, "height": a.height, "max_depth": a.depth,
                        "rays_per_frame": rays_per_frame, "tris": sd.ntri, "poses": a.poses,
-                       "parallelism": f"screen tiles x{world}" + (" + rccl gather" if world > 1 else "")},
+                       "parallelism": f"screen tiles x{world}" + (f" + {'rccl' if a.dist_backend == 'nccl' else 'gloo'} gather"
+                                                                   if world > 1 else "")},
             "kernel_ms_mean": round(float(kms.mean()), 4),
             "kernel_mrays_per_s": round(rays_per_frame / world / (kms.mean() * 1e-3) / 1e6, 2),
             "roofline": roof,

@@ -5,6 +5,11 @@ import sys
 
 import pytest
 
+try:  # torch first: libvrt.so then binds to torch's HIP runtime (one runtime
+    import torch  # noqa: F401  per process; see DESIGN.md "Host runtime")
+except Exception:  # pragma: no cover - CPU-only environments without torch
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 sys.path.insert(0, ROOT)
