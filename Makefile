@@ -42,6 +42,13 @@ $(PKG)/libvrt.so: $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# A/B variant of the kernels:  make variant NAME=v0 DEFS="-DVRT_EXPAND_V=0"
+variant: $(BLD)/vrt_host.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o | $(BLD)
+	mkdir -p build/variants
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
+	  build/variants/k_$(NAME).o $(BLD)/vrt_host.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o -lpthread
+
 # ISA listing + register/occupancy report of the kernels (for DESIGN.md)
 isa: | $(BLD)
 	$(HIPCC) $(HIPFLAGS) --offload-device-only -S $(SRC)/vrt_kernels.hip -o $(BLD)/vrt_kernels.s \

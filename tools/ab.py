@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""A/B timing of libvrt.so build variants in ONE process, interleaved rounds
+(cdna_hip_programming.md §5.4 rule 24).  Each variant library is loaded with
+its own ctypes handle; every variant's image must be bit-identical to the
+first one's (the baseline) or the run fails.
+
+usage: tools/ab.py lib1.so lib2.so ... [--rounds 6] [--width 1920 --height 1080 --depth 8]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch  # one HIP runtime: torch's
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import voxelraytrace20190722_amd as vrt  # noqa: E402
+from voxelraytrace20190722_amd import _ffi  # noqa: E402
+
+
+def load(path):
+    L = C.CDLL(os.path.abspath(path))
+    for name, (res, args) in _ffi.SIGNATURES.items():
+        if hasattr(L, name):
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--poses", type=int, default=16)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--detail", type=float, default=1.0)
+    a = ap.parse_args()
+    sd = vrt.SceneData.proxy(a.detail, 1)
+    film = _ffi.Film(1.0, 1.0, a.width, a.height)
+    libs = [load(p) for p in a.libs]
+    scenes = []
+    for L in libs:
+        h = C.c_void_p()
+        d = sd.desc()
+        rc = L.vrt_scene_create(C.byref(d), a.depth, 0, C.byref(h))
+        assert rc == 0, L.vrt_last_error()
+        scenes.append(h)
+    info = _ffi.SceneInfo()
+    libs[0].vrt_scene_info(scenes[0], C.byref(info))
+    cams = []
+    for i in range(a.poses):
+        fov, eye, spot, up = vrt.sweep_pose(info.root_min[:], info.root_max[:], i, a.poses)
+        cam = _ffi.Camera()
+        libs[0].vrt_camera_init(fov, eye.ctypes.data_as(_ffi.f32p), spot.ctypes.data_as(_ffi.f32p),
+                                up.ctypes.data_as(_ffi.f32p), 0.0, vrt.FLT_MAX, C.byref(cam))
+        cams.append(cam)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream(dev)
+    imgs = [torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev) for _ in libs]
+    times = {p: [] for p in a.libs}
+    ref = None
+    for r in range(a.rounds + 1):
+        for vi, (L, h, p) in enumerate(zip(libs, scenes, a.libs)):
+            evs = []
+            for ci, cam in enumerate(cams):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                rc = L.vrt_render_tiles_device(h, C.byref(cam), C.byref(film), 0, 1, 1,
+                                               C.c_void_p(imgs[vi].data_ptr()), C.c_void_p(st.cuda_stream))
+                assert rc == 0, L.vrt_last_error()
+                e1.record(st)
+                evs.append((e0, e1))
+                if r == 0 and ci == a.poses - 1:
+                    torch.cuda.synchronize()
+                    im = imgs[vi].cpu().numpy().view(np.uint32)
+                    if ref is None:
+                        ref = im
+                    elif not np.array_equal(im, ref):
+                        raise SystemExit(f"variant {p} differs from baseline {a.libs[0]}")
+            torch.cuda.synchronize()
+            if r > 0:  # round 0 = warm-up + parity
+                times[p].append(sum(s.elapsed_time(e) for s, e in evs) / len(evs))
+    base = np.median(times[a.libs[0]])
+    out = {}
+    for p in a.libs:
+        t = np.array(times[p])
+        out[os.path.basename(p)] = {"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
+                                    "speedup": round(float(base / np.median(t)), 3),
+                                    "mrays": round(a.width * a.height * 4 / np.median(t) / 1e3, 1)}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -458,6 +458,27 @@ static int build_tree(vrt_scene *s, const vrt_scene_desc *d)
                 if (l < D && lv_begin == lv_end)
                         break;
         }
+        // content masks, bottom-up (children always follow their parent):
+        // an internal node's b = the children that hold triangles somewhere
+        // below.  The kernels never push a child outside this mask: a
+        // subtree without triangles cannot hit, so the DFS result is
+        // unchanged (the instrumented kernel ignores it to count exactly the
+        // reference's visits).
+        {
+                std::vector<uint8_t> has((size_t)nnodes, 0);
+                for (int64_t ni = nnodes - 1; ni >= 0; --ni) {
+                        NodeRec &nr = s->nodes[ni];
+                        if (nr.a & kLeafBit) {
+                                has[ni] = (nr.a & ~kLeafBit) ? 1 : 0;
+                        } else {
+                                uint32_t m = 0;
+                                for (int c = 0; c < 8; ++c)
+                                        m |= (uint32_t)has[nr.a + c] << c;
+                                nr.b = m;
+                                has[ni] = m ? 1 : 0;
+                        }
+                }
+        }
         for (size_t i = 0; i < refs.size(); ++i) {
                 const uint32_t t = (uint32_t)(refs[i] & 0xFFFFFFFFu);
                 RefRec &rr = s->refs[i];
@@ -562,6 +583,14 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         s->dev.max_depth = s->max_depth;
         s->dev.nmat = (int32_t)s->mats.size();
         s->dev.ntex = (int32_t)s->texs.size();
+        {
+                bool ok = true;
+                for (int k = 0; k < 3; ++k) {
+                        const float lo = s->info.root_min[k], hi = s->info.root_max[k];
+                        ok = ok && std::fabs(lo) < 1.2676506e30f && std::fabs(hi) < 1.2676506e30f;
+                }
+                s->dev.fast_ok = ok ? 1 : 0;
+        }
         s->info.device_bytes = (int64_t)tot;
         HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreate(&s->ev0));

@@ -46,13 +46,125 @@ __device__ __forceinline__ void load_node(const NodeRec *__restrict__ nodes,
         b = __float_as_uint(q1.w);
 }
 
+#ifndef VRT_EXPAND_V
+#define VRT_EXPAND_V 1
+#endif
+
 // Expand an internal node with box [bmin,bmax]: slab-test its 8 children
 // (boxes from split()'s exact arithmetic) and return the hit children in
 // travorder order, 3 bits each (first child in bits 0-2); cnt = number.
 // full_pos (instrumented only): 3-bit position of each child ci (bits 3ci)
 // in the full 8-child travorder order, for the reference's test counts.
+//
+// kFast (chosen per wave when every lane's ray and the scene are finite and
+// no direction component is a non-zero denormal): no slab distance can be
+// NaN, so IEEE min/max (v_min/v_max/v_min3/v_max3) give the same values as
+// std::min/max and max_element/min_element up to the sign of a zero, which
+// no later comparison can observe.  The exact path keeps the reference's
+// select semantics for everything else.
+template <bool kFullPos, bool kFast>
+__device__ __forceinline__ uint32_t expand_v1(const float bmin[3],
+                                              const float bmax[3],
+                                              const RayK &r, int &cnt,
+                                              uint32_t &full_pos,
+                                              uint32_t content)
+{
+        const float oo[3] = { r.o.x, r.o.y, r.o.z };
+        const float dd[3] = { r.d.x, r.d.y, r.d.z };
+        const float di[3] = { r.dinv.x, r.dinv.y, r.dinv.z };
+        float nr[3][2], fr[3][2], q[3][2];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+                // split(): mask-0 child [min + 0*h, min + 0*h + h], mask-1
+                // child [min + h, min + h + h].  With a finite h (fast
+                // path: finite scene), min + 0*h and (min+0*h)+h equal min
+                // and min+h up to the sign of a zero, which no slab
+                // comparison or distance order can observe, so the planes
+                // are min, b = min+h, c = b+h.
+                const float h = (bmax[k] - bmin[k]) / 2.0f;
+                const float a0 = kFast ? bmin[k] : bmin[k] + 0.0f * h;
+                const float b = bmin[k] + h;
+                const float a1 = kFast ? b : a0 + h;
+                const float c = b + h;
+                const float ta = (a0 - oo[k]) * di[k];
+                const float tb0 = (a1 - oo[k]) * di[k];
+                const float tb1 = kFast ? tb0 : (b - oo[k]) * di[k];
+                const float tc = (c - oo[k]) * di[k];
+                if (kFast) {
+                        nr[k][0] = fminf(ta, tb0);
+                        fr[k][0] = fmaxf(ta, tb0);
+                        nr[k][1] = fminf(tb1, tc);
+                        fr[k][1] = fmaxf(tb1, tc);
+                } else {
+                        nr[k][0] = std_min(ta, tb0);
+                        fr[k][0] = std_max(ta, tb0);
+                        nr[k][1] = std_min(tb1, tc);
+                        fr[k][1] = std_max(tb1, tc);
+                }
+                q[k][0] = dd[k] * ((a0 + a1) * .5f - oo[k]);
+                q[k][1] = dd[k] * ((b + c) * .5f - oo[k]);
+        }
+        const float qx0 = 0.0f + q[0][0], qx1 = 0.0f + q[0][1];
+        float dist[8];
+        bool hit[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+                const int mx = (i >> 2) & 1, my = (i >> 1) & 1, mz = i & 1;
+                float t0, t1;
+                if (kFast) {
+                        t0 = fmaxf(fmaxf(nr[0][mx], nr[1][my]), nr[2][mz]);
+                        t1 = fminf(fminf(fr[0][mx], fr[1][my]), fr[2][mz]);
+                } else {
+                        t0 = nr[0][mx];
+                        t1 = fr[0][mx];
+                        if (t0 < nr[1][my]) t0 = nr[1][my];
+                        if (t0 < nr[2][mz]) t0 = nr[2][mz];
+                        if (fr[1][my] < t1) t1 = fr[1][my];
+                        if (fr[2][mz] < t1) t1 = fr[2][mz];
+                }
+                // !(t0 > t1) && (t0 in [tmin,tmax] || t1 in [tmin,tmax]),
+                // evaluated without branches
+                hit[i] = ((content >> i) & 1u) & !(t0 > t1) & (((t0 >= r.tmin) & (t0 <= r.tmax)) |
+                                       ((t1 >= r.tmin) & (t1 <= r.tmax)));
+                dist[i] = ((mx ? qx1 : qx0) + q[1][my]) + q[2][mz];
+        }
+        // rank of each hit child among the hit children under the stable
+        // (dist, index) order: j < i precedes i  <=>  !(dist_i < dist_j)
+        uint32_t rk[8], fp[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+                rk[i] = 0;
+                fp[i] = 0;
+        }
+#pragma unroll
+        for (int i = 1; i < 8; ++i) {
+#pragma unroll
+                for (int j = 0; j < i; ++j) {
+                        const bool c = dist[i] < dist[j];  // i strictly first
+                        rk[j] += (uint32_t)(c & hit[i]);
+                        rk[i] += (uint32_t)(!c & hit[j]);
+                        if (kFullPos) {
+                                fp[j] += (uint32_t)c;
+                                fp[i] += (uint32_t)!c;
+                        }
+                }
+        }
+        uint32_t order = 0;
+        int n = 0;
+        full_pos = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+                order |= hit[i] ? ((uint32_t)i << (3 * rk[i])) : 0u;
+                n += hit[i] ? 1 : 0;
+                if (kFullPos)
+                        full_pos |= fp[i] << (3 * i);
+        }
+        cnt = n;
+        return order;
+}
+
 template <bool kFullPos>
-__device__ __forceinline__ uint32_t expand(const float bmin[3],
+__device__ __forceinline__ uint32_t expand_v0(const float bmin[3],
                                            const float bmax[3],
                                            const RayK &r, int &cnt,
                                            uint32_t &full_pos)
@@ -123,6 +235,19 @@ __device__ __forceinline__ uint32_t expand(const float bmin[3],
         return order;
 }
 
+template <bool kFullPos, bool kFast>
+__device__ __forceinline__ uint32_t expand(const float bmin[3],
+                                           const float bmax[3],
+                                           const RayK &r, int &cnt,
+                                           uint32_t &full_pos, uint32_t content)
+{
+#if VRT_EXPAND_V == 0
+        return expand_v0<kFullPos>(bmin, bmax, r, cnt, full_pos);
+#else
+        return expand_v1<kFullPos, kFast>(bmin, bmax, r, cnt, full_pos, content);
+#endif
+}
+
 struct MarchResult {
         bool hit;
         uint32_t node;  // hit leaf
@@ -173,7 +298,7 @@ __device__ __forceinline__ bool leaf_isect(const RefRec *__restrict__ refs,
 
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).
-template <bool kCount>
+template <bool kCount, bool kFast>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint32_t *stk_base,
                                           uint32_t *stk_ord,
@@ -201,7 +326,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         }
         int cnt;
         uint32_t fpos;
-        uint32_t order = expand<kCount>(bmin, bmax, r, cnt, fpos);
+        uint32_t order = expand<kCount, kFast>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
         uint32_t base = a;
         uint32_t depth = 1;  // depth of the node whose children we walk
         uint32_t nexp = 1;
@@ -237,7 +362,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                         stk_aux[sp * kBlock] = fpos | (depth << 24);
                                 ++sp;
                         }
-                        order = expand<kCount>(bmin, bmax, r, cnt, fpos);
+                        order = expand<kCount, kFast>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
                         base = a;
                         ++depth;
                         ++nexp;
@@ -272,6 +397,32 @@ __device__ __forceinline__ RayK make_rayk(f3 o, f3 dn, float tmin, float tmax)
         r.tmin = tmin;
         r.tmax = tmax;
         return r;
+}
+
+// Rays for which expand's fast path is exact (see expand_v1): finite
+// origin and direction, no non-zero denormal direction component, and
+// coordinates far from overflow (the scene's own flag covers the boxes).
+__device__ __forceinline__ bool fast_ok(const RayK &r)
+{
+        const float lim = 1.2676506e30f;  // 2^100
+        bool ok = fabsf(r.o.x) < lim && fabsf(r.o.y) < lim && fabsf(r.o.z) < lim;
+        const float d[3] = { r.d.x, r.d.y, r.d.z };
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+                ok = ok && (d[k] == 0.f || (fabsf(d[k]) >= kFltMin && fabsf(d[k]) <= kFltMax));
+        return ok;
+}
+
+template <bool kCount>
+__device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const RayK &r,
+                                                   uint32_t *sb, uint32_t *so,
+                                                   uint32_t *sa, uint32_t *pr,
+                                                   MarchResult &m)
+{
+        if (__all(sc.fast_ok && fast_ok(r)))
+                ray_march<kCount, true>(sc, r, sb, so, sa, pr, m);
+        else
+                ray_march<kCount, false>(sc, r, sb, so, sa, pr, m);
 }
 
 // Triangle::get_diffuse(isect, ray, (1,1,1)) (VRT/voxel_octree.cc:462-484)
@@ -325,7 +476,10 @@ __device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
 // Primary render: one workgroup per 8x8 tile.
 // ---------------------------------------------------------------------------
 template <bool kCount>
-__global__ __launch_bounds__(kBlock) void k_render(RenderParams p)
+#ifndef VRT_WAVES_PER_EU
+#define VRT_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(kBlock, VRT_WAVES_PER_EU) void k_render(RenderParams p)
 {
         __shared__ uint32_t stk_base[kStack * kBlock];
         __shared__ uint32_t stk_ord[kStack * kBlock];
@@ -362,7 +516,7 @@ __global__ __launch_bounds__(kBlock) void k_render(RenderParams p)
                                  dn, c.tmin, c.tmax);
 
         MarchResult m;
-        ray_march<kCount>(p.sc, r, stk_base + tid, stk_ord + tid,
+        ray_march_dispatch<kCount>(p.sc, r, stk_base + tid, stk_ord + tid,
                           stk_aux + (kCount ? tid : 0),
                           path_rem + (kCount ? tid : 0), m);
 
@@ -433,7 +587,7 @@ __global__ __launch_bounds__(kBlock) void k_ray_march(DevScene sc,
         const RayK r = make_rayk(mk3(rr[0], rr[1], rr[2]), mk3(rr[3], rr[4], rr[5]),
                                  rr[6], rr[7]);
         MarchResult m;
-        ray_march<false>(sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false>(sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
         uint32_t *o = out + 9 * i;
         if (m.hit) {
                 f3 nrm;
