@@ -257,9 +257,95 @@ struct MarchResult {
         uint32_t A, L, T;  // reference-equivalent counters (instrumented)
 };
 
-// ray_march_isect (VRT/voxel_octree.cc:99-129) over one leaf's records.
+#ifndef VRT_LEAF_V
+#define VRT_LEAF_V 2
+#endif
+
+// ray_march_isect (VRT/voxel_octree.cc:99-129) over one leaf's records, with
+// intersect_triangle3 (VRT/raytri.cc:197-249) inlined in a register-frugal
+// order.  Every value is the same IEEE double operation on the same
+// operands as mt_isect(); only the evaluation order of independent terms
+// differs, and inv_det = 1.0/det -- side-effect free -- is evaluated only
+// for a triangle that passes every test, so the results are identical.
+// The best hit keeps (float)t; ISect::hit = o + (float)t*d is rebuilt once.
+template <bool kCount>
+__device__ __forceinline__ bool leaf_isect_v2(const RefRec *__restrict__ refs,
+                                              uint32_t first, uint32_t n,
+                                              const RayK &r, MarchResult &m)
+{
+        bool any = false;
+        float best = 0.f, best_t = 0.f;
+#pragma unroll 1
+        for (uint32_t k = 0; k < n; ++k) {
+                const float4 *q = reinterpret_cast<const float4 *>(refs + first + k);
+                const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+                const double v0x = q0.x, v0y = q0.y, v0z = q0.z;
+                const double dx = r.d.x, dy = r.d.y, dz = r.d.z;
+                // edge2, pvec = dir x edge2
+                const double e2x = (double)q1.z - v0x, e2y = (double)q1.w - v0y, e2z = (double)q2.x - v0z;
+                const double px = dy * e2z - dz * e2y;
+                const double py = dz * e2x - dx * e2z;
+                const double pz = dx * e2y - dy * e2x;
+                // edge1, det
+                const double e1x = (double)q0.w - v0x, e1y = (double)q1.x - v0y, e1z = (double)q1.y - v0z;
+                const double det = e1x * px + e1y * py + e1z * pz;
+                if (!(det > 0.000001) && !(det < -0.000001))
+                        continue;  // parallel
+                const double tx = (double)r.o.x - v0x, ty = (double)r.o.y - v0y, tz = (double)r.o.z - v0z;
+                const double uu = tx * px + ty * py + tz * pz;
+                const bool pos = det > 0.000001;
+                if (pos ? (uu < 0.0 || uu > det) : (uu > 0.0 || uu < det))
+                        continue;
+                const double qx = ty * e1z - tz * e1y;
+                const double qy = tz * e1x - tx * e1z;
+                const double qz = tx * e1y - ty * e1x;
+                const double vv = dx * qx + dy * qy + dz * qz;
+                if (pos ? (vv < 0.0 || uu + vv > det) : (vv > 0.0 || uu + vv < det))
+                        continue;
+                const double inv_det = 1.0 / det;
+                const double t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
+                // Triangle::isect (VRT/voxel_octree.cc:449-454)
+                const float fu = clampf((float)(uu * inv_det), 0, 1);
+                const float fv = clampf((float)(vv * inv_det), 0, 1);
+                const float tf = (float)t;
+                const f3 hp = r.o + r.d * tf;
+                const float depth = length(hp - r.o);
+                if (!any || depth < best) {  // min_element: first strict minimum
+                        any = true;
+                        best = depth;
+                        best_t = tf;
+                        m.tri = __float_as_uint(q2.y);
+                        m.u = fu;
+                        m.v = fv;
+                }
+        }
+        if (any)
+                m.hp = r.o + r.d * best_t;
+        if (kCount)
+                m.T += n;
+        return any;
+}
+
+template <bool kCount>
+__device__ __forceinline__ bool leaf_isect_v1(const RefRec *__restrict__ refs,
+                                              uint32_t first, uint32_t n,
+                                              const RayK &r, MarchResult &m);
+
 template <bool kCount>
 __device__ __forceinline__ bool leaf_isect(const RefRec *__restrict__ refs,
+                                           uint32_t first, uint32_t n,
+                                           const RayK &r, MarchResult &m)
+{
+#if VRT_LEAF_V == 2
+        return leaf_isect_v2<kCount>(refs, first, n, r, m);
+#else
+        return leaf_isect_v1<kCount>(refs, first, n, r, m);
+#endif
+}
+
+// (v1: straight call of the shared mt_isect)
+template <bool kCount>
+__device__ __forceinline__ bool leaf_isect_v1(const RefRec *__restrict__ refs,
                                            uint32_t first, uint32_t n,
                                            const RayK &r, MarchResult &m)
 {
@@ -331,6 +417,70 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         uint32_t depth = 1;  // depth of the node whose children we walk
         uint32_t nexp = 1;
         int sp = 0;
+#ifndef VRT_WHILE_WHILE
+#define VRT_WHILE_WHILE 1
+#endif
+#if VRT_WHILE_WHILE
+        // while-while: every lane first advances (pop / expand) to its next
+        // non-empty leaf in DFS order, then the lanes test their leaves
+        // together -- expand and leaf code no longer interleave per lane.
+        for (;;) {
+                bool leaf = false;
+                uint32_t node = 0, nref = 0;
+                for (;;) {
+                        if (cnt == 0) {
+                                if (sp == 0)
+                                        break;
+                                --sp;
+                                base = stk_base[sp * kBlock];
+                                const uint32_t w = stk_ord[sp * kBlock];
+                                order = w & 0xFFFFFFu;
+                                cnt = (int)(w >> 24);
+                                if (kCount) {
+                                        const uint32_t x = stk_aux[sp * kBlock];
+                                        fpos = x & 0xFFFFFFu;
+                                        depth = x >> 24;
+                                }
+                                continue;
+                        }
+                        const uint32_t ci = order & 7u;
+                        order >>= 3;
+                        --cnt;
+                        node = base + ci;
+                        if (kCount)
+                                path_rem[depth * kBlock] = 7u - ((fpos >> (3 * ci)) & 7u);
+                        load_node(sc.nodes, node, bmin, bmax, a, b);
+                        if (!(a & kLeafBit)) {
+                                if (cnt) {
+                                        stk_base[sp * kBlock] = base;
+                                        stk_ord[sp * kBlock] = order | ((uint32_t)cnt << 24);
+                                        if (kCount)
+                                                stk_aux[sp * kBlock] = fpos | (depth << 24);
+                                        ++sp;
+                                }
+                                order = expand<kCount, kFast>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
+                                base = a;
+                                ++depth;
+                                ++nexp;
+                                continue;
+                        }
+                        if (kCount)
+                                m.L++;
+                        nref = a & ~kLeafBit;
+                        if (nref == 0)
+                                continue;  // empty leaf (instrumented walk only)
+                        leaf = true;
+                        break;
+                }
+                if (!leaf)
+                        break;
+                if (leaf_isect<kCount>(sc.refs, b, nref, r, m)) {
+                        m.hit = true;
+                        m.node = node;
+                        break;
+                }
+        }
+#else
         for (;;) {
                 if (cnt == 0) {
                         if (sp == 0)
@@ -377,6 +527,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         break;
                 }
         }
+#endif
         if (kCount) {
                 // 1 root test + 8 per expanded node, minus the children the
                 // reference never popped on the path it stopped on.
@@ -477,7 +628,9 @@ __device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
 // ---------------------------------------------------------------------------
 template <bool kCount>
 #ifndef VRT_WAVES_PER_EU
-#define VRT_WAVES_PER_EU 1
+// 6 waves per SIMD (80 VGPRs, a 32-B/lane spill) measured 8% faster than
+// the unconstrained 4 waves/SIMD (99 VGPRs): the march is latency-bound.
+#define VRT_WAVES_PER_EU 6
 #endif
 __global__ __launch_bounds__(kBlock, VRT_WAVES_PER_EU) void k_render(RenderParams p)
 {
