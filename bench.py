@@ -51,6 +51,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-counters", action="store_true")
+    p.add_argument("--mode", default="primary", choices=["primary", "secondary"],
+                   help="primary: BASELINE configs 1-4 (4 spp primary render); secondary: config 5")
+    p.add_argument("--spp", type=int, default=64, help="secondary rays per hit pixel (--mode secondary)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (RCCL over xGMI, the real path) or gloo (host-staged rehearsal)")
     p.add_argument("--save-image", default="", help="rank 0 writes the last frame as .hdr")
@@ -95,8 +98,18 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     tpr = vrt.tiles_per_rank(film, world)
-    img = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev)
-    if world > 1:
+    secondary = a.mode == "secondary"
+    img = torch.zeros((a.height, a.width) if secondary else (a.height, a.width, 3), dtype=torch.float32,
+                      device=dev)
+    if secondary:
+        # config 5: rays per frame are data dependent (64 per primary hit):
+        # count them per pose once, outside the timed region
+        frame_rays = {}
+        for pi in sorted({k % a.poses for k in range(a.steps)}):
+            _, frame_rays[pi] = tree.render_secondary(cams[pi], film, spp=a.spp)
+        prim = torch.zeros(W8 * H8 * 8, dtype=torch.float32, device=dev)
+        visb = [torch.zeros((a.height, a.width), dtype=torch.float32, device=dev) for _ in range(2)]
+    elif world > 1:
         # double-buffered: the RCCL gather of frame k (on the NCCL stream)
         # overlaps the render of frame k+1 (on the compute stream)
         tiles = [torch.zeros(tpr * 192, dtype=torch.float32, device=dev) for _ in range(2)]
@@ -111,12 +124,44 @@ def main():
         """Rank 0: re-assemble the frame gathered into buffer b."""
         if works[b] is None:
             return
-        works[b].wait()  # stream-wait on the gather, no host block
+        works[b].wait()  # stream-wait on the collective, no host block
         works[b] = None
         if rank == 0:
-            vrt.unpack_tiles_device(film, world, gathered[b].data_ptr(), img.data_ptr(), sp)
+            if secondary:
+                img.copy_(visb[b])
+            else:
+                vrt.unpack_tiles_device(film, world, gathered[b].data_ptr(), img.data_ptr(), sp)
+
+    def step_secondary(k, timed):
+        cam = cams[k % a.poses]
+        if timed:
+            ev[k][0].record(stream)
+        if world == 1:
+            tree.render_secondary_device(cam, film, a.spp, 0, 1, prim.data_ptr(), img.data_ptr(), sp)
+            if timed:
+                ev[k][1].record(stream)
+            return
+        b = k & 1
+        finish(b)
+        if rank == 0:
+            visb[b].zero_()  # the previous reduce summed into rank 0's buffer
+        # each rank writes only its own pixels (64-pixel chunks, round-robin);
+        # the others stay +0.0, so a SUM reduce assembles the image exactly
+        tree.render_secondary_device(cam, film, a.spp, rank, world, prim.data_ptr(), visb[b].data_ptr(), sp)
+        if timed:
+            ev[k][1].record(stream)
+        finish(1 - b)
+        if a.dist_backend == "nccl":
+            works[b] = dist.reduce(visb[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
+        else:
+            host = visb[b].cpu()
+            dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                img.copy_(host)
 
     def step(k, timed):
+        if secondary:
+            return step_secondary(k, timed)
         cam = cams[k % a.poses]
         if timed:
             ev[k][0].record(stream)
@@ -170,7 +215,7 @@ def main():
     # ---- algorithmic bytes from the instrumented kernel's
     # reference-equivalent counters, per pose actually rendered
     roof = None
-    if not a.no_counters:
+    if not a.no_counters and not secondary:
         poses_used = sorted({k % a.poses for k in range(a.steps)})
         b_rank = []
         cnt_tot = np.zeros(4)
@@ -208,7 +253,7 @@ def main():
     # ---- CPU baseline: the oracle (C restatement of the reference path,
     # render_mt-style 8x8 tiles over pthreads) on a bounded row sample
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu:
+    if rank == 0 and world == 1 and not a.no_cpu and not secondary:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle as po
         osc = po.Scene(sd, a.depth)
@@ -234,22 +279,37 @@ def main():
     if rank == 0 and a.save_image:
         vrt.write_hdr(a.save_image, img.cpu().numpy())
     if rank == 0:
-        total_rays = rays_per_frame * a.steps
+        coll = "rccl" if a.dist_backend == "nccl" else "gloo"
+        n_side = int(round(2 ** a.depth))
+        if secondary:
+            per_step = [frame_rays[k % a.poses] for k in range(a.steps)]
+            total_rays = int(sum(per_step))
+            mean_rays = total_rays / a.steps
+            metric = (f"Mrays/s at {a.width}x{a.height} Sponza {n_side}^3 octree "
+                      f"(1 primary + {a.spp} stochastic secondary rays per hit pixel)")
+            workload = (f"config 5: {a.width}x{a.height} primary hit + {a.spp} spp secondary rays, "
+                        f"sponza-proxy ({sd.ntri} tris), max_depth {a.depth}")
+            par = f"pixel chunks x{world}" + (f" + {coll} sum-reduce" if world > 1 else "")
+        else:
+            total_rays = rays_per_frame * a.steps
+            mean_rays = rays_per_frame
+            metric = f"Mrays/s at {a.width}x{a.height} Sponza {n_side}^3 octree (primary rays, 4 spp)"
+            workload = (f"primary render {a.width}x{a.height} x4 spp, sponza-proxy ({sd.ntri} tris), "
+                        f"max_depth {a.depth} (\"{n_side}^3\")")
+            par = f"screen tiles x{world}" + (f" + {coll} gather" if world > 1 else "")
         value = total_rays / elapsed / 1e6
         out = {
-            "metric": "Mrays/s at 1920x1080 Sponza 256^3 octree (primary rays, 4 spp)",
+            "metric": metric,
             "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32+f64",
             "data": "synthetic: deterministic sponza-proxy atrium (sponza.obj absent), 16-pose camera sweep",
-            "config": {"workload": f"primary render {a.width}x{a.height} x4 spp, sponza-proxy "
-                                   f"({sd.ntri} tris), max_depth {a.depth} (\"256^3\")",
+            "config": {"workload": workload, "mode": a.mode,
                        "width": a.width, "height": a.height, "max_depth": a.depth,
-                       "rays_per_frame": rays_per_frame, "tris": sd.ntri, "poses": a.poses,
-                       "parallelism": f"screen tiles x{world}" + (f" + {'rccl' if a.dist_backend == 'nccl' else 'gloo'} gather"
-                                                                   if world > 1 else "")},
+                       "rays_per_frame": int(round(mean_rays)), "tris": sd.ntri, "poses": a.poses,
+                       "parallelism": par},
             "kernel_ms_mean": round(float(kms.mean()), 4),
-            "kernel_mrays_per_s": round(rays_per_frame / world / (kms.mean() * 1e-3) / 1e6, 2),
+            "kernel_mrays_per_s": round(mean_rays / world / (kms.mean() * 1e-3) / 1e6, 2),
             "roofline": roof,
             "cpu_baseline": cpu,
         }

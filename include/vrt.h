@@ -169,6 +169,29 @@ int vrt_unpack_tiles_device(const vrt_film *film, int nranks,
  * (HIP events around the launch, on its stream). */
 int vrt_last_kernel_ms(vrt_scene *s, float *ms);
 
+/* SURVEY §8(d) config 5 (stochastic secondary rays, divergent traversal):
+ * per pixel of the 8*(n/8) render area a pixel-centre primary ray
+ * (gen_rays1); on a hit, jql::PCG seeded 0xc01dbeef ^ (py*nx+px) draws `spp`
+ * (1..64) points with jql::random_point_in_unit_sphere (libstdc++'s
+ * uniform_real_distribution<float>{-1,1} mapping) and each traces
+ * Ray{isect.hit, isect.normal + p, res, FLT_MAX} (VRT/voxel_octree.cc:
+ * 600-603 pattern; res = min(root.size()/2^max_depth), VRT/main.cc:69-70).
+ * vis[py*nx+px] = misses/spp (1 on a primary miss, 0 outside the area).
+ * Per-ray ids (index (py*nx+px)*spp + s) may be NULL; *rays (may be NULL)
+ * = rays traced (primary + secondary). */
+int vrt_render_secondary(vrt_scene *s, const vrt_camera *cam,
+                         const vrt_film *film, int spp, float *vis,
+                         int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox,
+                         int64_t *rays);
+/* Device-resident variant: rank `rank` of `nranks` writes its pixels (64-
+ * pixel chunks dealt round-robin) into d_vis (nx*ny floats, caller-zeroed:
+ * a sum-reduce over ranks assembles the image exactly); d_prim = scratch of
+ * 8*(nx/8)*8*(ny/8)*8 floats. */
+int vrt_render_secondary_device(vrt_scene *s, const vrt_camera *cam,
+                                const vrt_film *film, int spp, int rank,
+                                int nranks, float *d_prim, float *d_vis,
+                                void *stream);
+
 /* Batched gi::ray_march (VRT/voxel_octree.cc:131-188) on host arrays. */
 int vrt_ray_march_batch(vrt_scene *s, const vrt_ray *rays, int64_t n,
                         vrt_hit *hits);

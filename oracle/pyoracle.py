@@ -56,6 +56,11 @@ def oracle():
             "ora_render_rows": (C.c_double, [P, f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int,
                                              C.c_int, C.c_int, f32p]),
             "ora_linear_to_rgbe": (None, [f32p, u8p]),
+            "ora_pcg_next": (C.c_uint32, [C.POINTER(C.c_uint64)]),
+            "ora_uniform_m11": (C.c_float, [C.POINTER(C.c_uint64)]),
+            "ora_random_point_in_unit_sphere": (None, [C.POINTER(C.c_uint64), f32p]),
+            "ora_render_secondary": (C.c_int64, [P, f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int,
+                                                 C.c_int, f32p, i32p, i32p, u32p]),
         }
         for k, (res, args) in sig.items():
             f = getattr(L, k)
@@ -124,6 +129,19 @@ def ref_hdr_bytes(img):
     n2 = reference().ref_write_hdr_mem(w, h, comp, _p(img, f32p), _p(buf, u8p), -n)
     assert n2 == -n
     return buf.tobytes()
+
+
+def uniform_draws(seed, n):
+    st = C.c_uint64(seed)
+    return np.array([oracle().ora_uniform_m11(C.byref(st)) for _ in range(n)], np.float32)
+
+
+def sphere_points(seed, n):
+    st = C.c_uint64(seed)
+    out = np.zeros((n, 3), np.float32)
+    for i in range(n):
+        oracle().ora_random_point_in_unit_sphere(C.byref(st), _p(out[i], f32p))
+    return out
 
 
 # ---------------------------------------------------------------- camera
@@ -237,6 +255,17 @@ class Scene:
                             _p(so["voxel"], u32p) if so else None, _p(so["rgb"], f32p) if so else None,
                             _p(so["counters"], u32p) if so else None)
         return (rgb, so) if so else rgb
+
+    def render_secondary(self, cam, film_w, film_h, nx, ny, spp=64, nthreads=8, ids=True):
+        vis = np.zeros((ny, nx), np.float32)
+        ns = nx * ny * spp
+        d = {"hit": np.zeros(ns, np.int32), "tri": np.zeros(ns, np.int32),
+             "voxel": np.zeros(ns, np.uint32)} if ids else None
+        rays = oracle().ora_render_secondary(self.h, _p(cam, f32p), film_w, film_h, nx, ny, spp, nthreads,
+                                             _p(vis, f32p), _p(d["hit"], i32p) if d else None,
+                                             _p(d["tri"], i32p) if d else None,
+                                             _p(d["voxel"], u32p) if d else None)
+        return (vis, rays, d) if ids else (vis, rays)
 
     def render_rows(self, cam, film_w, film_h, nx, ny, row_stride, row_phase, nthreads):
         rgb = np.zeros((ny, nx, 3), np.float32)

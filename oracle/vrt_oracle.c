@@ -1013,3 +1013,148 @@ void ora_linear_to_rgbe(const float lin[3], uint8_t rgbe[4])
                 rgbe[3] = (unsigned char)(e + 128);
         }
 }
+
+/* ------------------------------------------------------------------ */
+/* Config 5: stochastic secondary rays                   */
+/* ------------------------------------------------------------------ */
+/* jql::PCG::operator() (VRT/graphics_math.h:836-849) */
+uint32_t ora_pcg_next(uint64_t *state)
+{
+        *state = *state * 6364136223846793005ULL + 1442695040888963407ULL;
+        const uint64_t s = *state;
+        const uint32_t xorshift = (uint32_t)((s ^ (s >> 18u)) >> 27u);
+        const uint64_t shift = s >> 59u;
+        const int32_t sh32 = (int32_t)(uint32_t)shift; /* reinterpret low 32 bits */
+        return (xorshift >> shift) | (xorshift << ((uint32_t)(-sh32) & 31u));
+}
+
+/* libstdc++ 11: generate_canonical<float, 24>(pcg) (random.tcc:3348-3380),
+ * then uniform_real_distribution<float>{-1,1}: (u * (b - a)) + a. */
+float ora_uniform_m11(uint64_t *state)
+{
+        float sum = 0.0f;
+        sum += (float)ora_pcg_next(state) * 1.0f;
+        float ret = sum / 4294967296.0f;
+        if (ret >= 1.0f)
+                ret = nextafterf(1.0f, 0.0f);
+        return (ret * (1.0f - -1.0f)) + -1.0f;
+}
+
+/* jql::random_point_in_unit_sphere (VRT/graphics_math.h:1208-1216): braced
+ * init evaluates d(pcg) left to right; accept when length(r) < 1. */
+void ora_random_point_in_unit_sphere(uint64_t *state, float p[3])
+{
+        for (;;) {
+                float x = ora_uniform_m11(state);
+                float y = ora_uniform_m11(state);
+                float z = ora_uniform_m11(state);
+                if (length(mk(x, y, z)) < 1.f) {
+                        p[0] = x;
+                        p[1] = y;
+                        p[2] = z;
+                        return;
+                }
+        }
+}
+
+typedef struct {
+        const ora_scene *s;
+        const float *cam;
+        float fw, fh, res;
+        int nx, ny, spp;
+        float *vis;
+        int32_t *s_hit, *s_tri;
+        uint32_t *s_vox;
+        atomic_int next_row;
+        atomic_llong rays;
+} sjob;
+
+static void *secondary_worker(void *arg)
+{
+        sjob *j = arg;
+        const int W8 = 8 * (j->nx / 8), H8 = 8 * (j->ny / 8);
+        for (;;) {
+                const int py = atomic_fetch_add(&j->next_row, 1);
+                if (py >= H8)
+                        break;
+                long long rays = 0;
+                for (int px = 0; px < W8; ++px) {
+                        float pr[8];
+                        ora_gen_rays1(j->cam, j->fw, j->fh, j->nx, j->ny, px, py, pr);
+                        omarch m;
+                        const size_t pi = (size_t)py * j->nx + px;
+                        ++rays;
+                        if (!ray_march(j->s, pr, &m)) {
+                                j->vis[pi] = 1.0f;
+                                continue;
+                        }
+                        uint64_t st = 0xc01dbeefULL ^ (uint64_t)((uint64_t)py * (uint64_t)j->nx + (uint64_t)px);
+                        int misses = 0;
+                        for (int s = 0; s < j->spp; ++s) {
+                                float p[3], r[8];
+                                ora_random_point_in_unit_sphere(&st, p);
+                                const float o[3] = { m.is.hit.x, m.is.hit.y, m.is.hit.z };
+                                const float d[3] = { m.is.normal.x + p[0], m.is.normal.y + p[1],
+                                                     m.is.normal.z + p[2] };
+                                ora_make_ray(o, d, j->res, FLT_MAX, r);
+                                omarch m2;
+                                const int h = ray_march(j->s, r, &m2);
+                                ++rays;
+                                misses += !h;
+                                const size_t si = pi * (size_t)j->spp + s;
+                                if (j->s_hit) j->s_hit[si] = h;
+                                if (j->s_tri) j->s_tri[si] = h ? m2.tri : -1;
+                                if (j->s_vox)
+                                        j->s_vox[si] = h ? vox_key(&j->s->nodes[m2.leaf]) : 0xFFFFFFFFu;
+                        }
+                        j->vis[pi] = (float)misses / (float)j->spp;
+                }
+                atomic_fetch_add(&j->rays, rays);
+        }
+        return NULL;
+}
+
+int64_t ora_render_secondary(const ora_scene *s, const float cam[19],
+                             float film_w, float film_h, int nx, int ny,
+                             int spp, int nthreads, float *vis,
+                             int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox)
+{
+        sjob j;
+        memset(&j, 0, sizeof j);
+        j.s = s;
+        j.cam = cam;
+        j.fw = film_w;
+        j.fh = film_h;
+        j.nx = nx;
+        j.ny = ny;
+        j.spp = spp;
+        j.vis = vis;
+        j.s_hit = s_hit;
+        j.s_tri = s_tri;
+        j.s_vox = s_vox;
+        /* Res = *min_element(root.aabb.size() / powf(2, D)) (VRT/main.cc:69-70) */
+        const float *rb = s->nodes[0].box;
+        const float p2 = powf(2.f, (float)s->max_depth);
+        float res = (rb[3] - rb[0]) / p2;
+        if ((rb[4] - rb[1]) / p2 < res) res = (rb[4] - rb[1]) / p2;
+        if ((rb[5] - rb[2]) / p2 < res) res = (rb[5] - rb[2]) / p2;
+        j.res = res;
+        memset(vis, 0, sizeof(float) * (size_t)nx * ny);
+        const size_t ns = (size_t)nx * ny * (size_t)spp;
+        if (s_hit) memset(s_hit, 0, sizeof(int32_t) * ns);
+        if (s_tri) for (size_t i = 0; i < ns; ++i) s_tri[i] = -1;
+        if (s_vox) for (size_t i = 0; i < ns; ++i) s_vox[i] = 0xFFFFFFFFu;
+        atomic_init(&j.next_row, 0);
+        atomic_init(&j.rays, 0);
+        if (nthreads <= 1) {
+                secondary_worker(&j);
+        } else {
+                pthread_t *th = malloc(sizeof(pthread_t) * (size_t)nthreads);
+                for (int i = 0; i < nthreads; ++i)
+                        pthread_create(&th[i], NULL, secondary_worker, &j);
+                for (int i = 0; i < nthreads; ++i)
+                        pthread_join(th[i], NULL);
+                free(th);
+        }
+        return (int64_t)atomic_load(&j.rays);
+}

@@ -109,6 +109,29 @@ double ora_render_rows(const ora_scene *s, const float cam[19], float film_w,
                        float film_h, int nx, int ny, int row_stride,
                        int row_phase, int nthreads, float *rgb);
 
+/* jql::PCG (VRT/graphics_math.h:821-857): one operator() call. */
+uint32_t ora_pcg_next(uint64_t *state);
+/* std::uniform_real_distribution<float>{-1, 1}(pcg) as libstdc++ 11 does it
+ * (generate_canonical<float,24>: one draw, float(g)/2^32 clamped below 1,
+ * then u*(b-a)+a; /usr/include/c++/11/bits/random.tcc:3348-3380,
+ * random.h:1868-1870). */
+float ora_uniform_m11(uint64_t *state);
+/* jql::random_point_in_unit_sphere (VRT/graphics_math.h:1208-1216). */
+void ora_random_point_in_unit_sphere(uint64_t *state, float p[3]);
+/* SURVEY §8(d) config 5 ("64 spp stochastic secondary rays"), over the
+ * 8*(n/8) render area: primary = gen_rays1 (pixel centre); on a hit, PCG
+ * seeded 0xc01dbeef ^ (py*nx+px) draws `spp` points p, secondary ray =
+ * Ray{isect.hit, isect.normal + p, res, FLT_MAX} (the ctor normalises; the
+ * pattern of VRT/voxel_octree.cc:600-603); vis[py*nx+px] = misses / spp
+ * (1 for a primary miss, 0 outside the render area).  res = min component
+ * of root.size() / 2^max_depth (VRT/main.cc:69-70).  Optional per-ray
+ * outputs (index (py*nx+px)*spp + s): s_hit, s_tri, s_vox (unused slots
+ * -1 / 0xFFFFFFFF).  Returns the number of rays traced. */
+int64_t ora_render_secondary(const ora_scene *s, const float cam[19],
+                             float film_w, float film_h, int nx, int ny,
+                             int spp, int nthreads, float *vis,
+                             int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox);
+
 /* stbiw__linear_to_rgbe (VRT/stb_image_write.h:601-616) for one pixel. */
 void ora_linear_to_rgbe(const float linear[3], uint8_t rgbe[4]);
 

@@ -135,6 +135,40 @@ def scene_fixture(name, sd, depth, cams, films):
     return rec
 
 
+def pcg_std():
+    """Draws of the real libstdc++ uniform_real_distribution<float> over the
+    jql::PCG engine (tests/golden/pcg_std.cpp compiled with g++)."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "pcg_std")
+        subprocess.run(["g++", "-O2", "-ffp-contract=off", "-o", exe, os.path.join(HERE, "pcg_std.cpp")],
+                       check=True)
+        out = subprocess.run([exe, "64", "48", "64"], check=True, capture_output=True, text=True).stdout
+    seeds, draws, pts = [], [], {}
+    for ln in out.splitlines():
+        f = ln.split()
+        if f[0] == "U":
+            seeds.append(int(f[1]))
+            draws.append([float.fromhex(x) for x in f[2:]])
+        else:
+            pts.setdefault(int(f[1]), []).append([float.fromhex(x) for x in f[2:5]])
+    return (np.array(seeds, np.uint64), np.array(draws, np.float32),
+            np.array([pts[s] for s in seeds], np.float32))
+
+
+def secondary_fixture(sd, depth, cam, film, spp, name):
+    osc = po.Scene(sd, depth)
+    c = po.camera(*cam)
+    vis, rays, d = osc.render_secondary(c, film[0], film[1], film[2], film[3], spp=spp, nthreads=8)
+    rec = {"pos": sd.pos, "nrm": sd.nrm, "uv": sd.uv, "mat": sd.mat, "mat_tex": sd.mat_tex,
+           "mat_kd": sd.mat_kd, "tex_dims": sd.tex_dims, "tex_off": sd.tex_off, "tex_data": sd.tex_data,
+           "depth": np.int32(depth), "cam": np.array([cam[0], *cam[1], *cam[2], *cam[3]], np.float32),
+           "film": np.array(film, np.float32), "spp": np.int32(spp), "vis": vis, "rays": np.int64(rays),
+           "hit": d["hit"], "tri": d["tri"], "voxel": d["voxel"]}
+    np.savez_compressed(os.path.join(HERE, f"secondary_{name}.npz"), **rec)
+
+
 def main():
     if not po.reference_available():
         raise SystemExit("oracle/_ref/libvrtref.so missing: run `make` where /root/reference exists")
@@ -161,6 +195,9 @@ def main():
                   [(vrt.to_radian(70), (0.1, 0.2, 2.8), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0)),
                    (vrt.to_radian(100), (0.05, 0.0, 0.02), (1.0, 0.3, 0.2), (0.0, 1.0, 0.0))],
                   [(1.0, 1.0, 40, 40), (1.0, 1.0, 33, 27)])
+    seeds, draws, pts = pcg_std()
+    np.savez_compressed(os.path.join(HERE, "pcg_std.npz"), seeds=seeds, draws=draws, points=pts)
+    secondary_fixture(sd, 6, main_cam, (1.0, 1.0, 24, 16), 64, "proxy")
     for f in sorted(os.listdir(HERE)):
         print(f, os.path.getsize(os.path.join(HERE, f)))
 

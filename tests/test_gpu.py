@@ -199,3 +199,51 @@ def test_edge_scenes():
     orgb = osc.render(po.camera(vrt.to_radian(60), (0, 0, 1), (0, 0, 0), (0, 1, 0)), 1.0, 1.0, 32, 32,
                       samples=False)
     assert np.array_equal(bits(rgb), bits(orgb))
+
+
+def test_secondary_matches_golden_fixture():
+    z = golden("secondary_proxy.npz")
+    tree = vrt.VoxelOctree(scene_from(z), int(z["depth"]))
+    c = z["cam"]
+    fw, fh, nx, ny = z["film"]
+    cam = vrt.Camera(float(c[0]), c[1:4], c[4:7], c[7:10])
+    vis, rays, d = tree.render_secondary(cam, vrt.Film(float(fw), float(fh), int(nx), int(ny)),
+                                         spp=int(z["spp"]), ids=True)
+    assert rays == int(z["rays"])
+    for k in ("hit", "tri", "voxel"):
+        assert np.array_equal(d[k], z[k]), k
+    assert np.array_equal(bits(vis), bits(z["vis"]))
+
+
+@pytest.mark.parametrize("spp", [1, 17, 64])
+def test_secondary_matches_oracle_live(proxy_small, spp):
+    tree = vrt.VoxelOctree(proxy_small, 7)
+    osc = po.Scene(proxy_small, 7)
+    mn, mx = tree.root_box
+    fov, eye, spot, up = vrt.sweep_pose(mn, mx, 9, 16)
+    film = vrt.Film(1, 1, 40, 24)
+    vis, rays, d = tree.render_secondary(vrt.Camera(fov, eye, spot, up), film, spp=spp, ids=True)
+    ovis, orays, od = osc.render_secondary(po.camera(fov, eye, spot, up), 1.0, 1.0, 40, 24, spp=spp)
+    assert rays == orays
+    for k in ("hit", "tri", "voxel"):
+        assert np.array_equal(d[k], od[k]), k
+    assert np.array_equal(bits(vis), bits(ovis))
+
+
+def test_secondary_rank_partition_sums_to_image(proxy_small):
+    import torch
+    tree = vrt.VoxelOctree(proxy_small, 6)
+    mn, mx = tree.root_box
+    fov, eye, spot, up = vrt.sweep_pose(mn, mx, 4, 16)
+    cam = vrt.Camera(fov, eye, spot, up)
+    film = vrt.Film(1, 1, 72, 40)
+    ref, _ = tree.render_secondary(cam, film, spp=64)
+    dev = torch.device("cuda:0")
+    prim = torch.zeros(72 * 40 * 8, dtype=torch.float32, device=dev)
+    acc = torch.zeros((40, 72), dtype=torch.float32, device=dev)
+    for r in range(3):
+        part = torch.zeros((40, 72), dtype=torch.float32, device=dev)
+        tree.render_secondary_device(cam, film, 64, r, 3, prim.data_ptr(), part.data_ptr(), None)
+        torch.cuda.synchronize()
+        acc += part
+    assert np.array_equal(bits(acc.cpu().numpy()), bits(ref))

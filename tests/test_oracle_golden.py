@@ -60,3 +60,25 @@ def test_oracle_ray_march_consistent_with_render():
     assert np.array_equal(r["voxel"], z["s0_voxel"])
     assert np.array_equal(r["counters"], z["s0_counters"])
     assert np.array_equal(sc.shade(rays).view(np.uint32), z["s0_rgb"].view(np.uint32))
+
+
+def test_oracle_pcg_matches_libstdcxx():
+    """jql::PCG + libstdc++'s uniform_real_distribution<float>{-1,1} and
+    random_point_in_unit_sphere: oracle draws == the real libstdc++ ones."""
+    z = golden("pcg_std.npz")
+    for s, dr, pt in zip(z["seeds"], z["draws"], z["points"]):
+        assert np.array_equal(po.uniform_draws(int(s), dr.shape[0]).view(np.uint32), dr.view(np.uint32))
+        assert np.array_equal(po.sphere_points(int(s), pt.shape[0]).view(np.uint32), pt.view(np.uint32))
+
+
+def test_oracle_secondary_matches_fixture():
+    z = golden("secondary_proxy.npz")
+    sc = po.Scene(scene_from(z), int(z["depth"]))
+    c = z["cam"]
+    fw, fh, nx, ny = (float(x) for x in z["film"])
+    vis, rays, d = sc.render_secondary(po.camera(float(c[0]), c[1:4], c[4:7], c[7:10]), fw, fh, int(nx), int(ny),
+                                       spp=int(z["spp"]), nthreads=3)
+    assert rays == int(z["rays"])
+    assert np.array_equal(vis.view(np.uint32), z["vis"].view(np.uint32))
+    for k in ("hit", "tri", "voxel"):
+        assert np.array_equal(d[k], z[k])

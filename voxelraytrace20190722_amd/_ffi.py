@@ -95,6 +95,10 @@ SIGNATURES = {
                                           C.c_int, C.c_int, _P, _P]),
     "vrt_unpack_tiles_device": (C.c_int, [C.POINTER(Film), C.c_int, _P, _P, _P]),
     "vrt_last_kernel_ms": (C.c_int, [_P, f32p]),
+    "vrt_render_secondary": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), C.c_int, f32p, i32p,
+                                       i32p, u32p, i64p]),
+    "vrt_render_secondary_device": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), C.c_int, C.c_int,
+                                              C.c_int, _P, _P, _P]),
     "vrt_ray_march_batch": (C.c_int, [_P, C.POINTER(Ray), C.c_int64, C.POINTER(Hit)]),
     "vrt_ray_march_batch_device": (C.c_int, [_P, _P, C.c_int64, _P, _P]),
     "vrt_device_selftest": (C.c_int, [C.c_int, f64p, f64p, f32p, i32p, C.c_int64]),

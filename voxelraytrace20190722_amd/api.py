@@ -232,6 +232,29 @@ class VoxelOctree:
                            "tri_tests": st.tri_tests, "hits": st.hits, "kernel_ms": st.kernel_ms}
         return (rgb, so) if so is not None else rgb
 
+    def render_secondary(self, cam, film, spp=64, ids=False):
+        """Config 5: per-pixel sky visibility from `spp` stochastic secondary
+        rays -> (ny, nx) float32 image, rays traced (+ per-ray id dict)."""
+        nx, ny = film.nx, film.ny
+        vis = np.zeros((ny, nx), np.float32)
+        rays = C.c_int64()
+        d = None
+        if ids:
+            ns = nx * ny * spp
+            d = {"hit": np.zeros(ns, np.int32), "tri": np.zeros(ns, np.int32), "voxel": np.zeros(ns, np.uint32)}
+        check(lib().vrt_render_secondary(self.h, C.byref(cam.c), C.byref(film.c), int(spp), ptr(vis, _ffi.f32p),
+                                         ptr(d["hit"], _ffi.i32p) if d else None,
+                                         ptr(d["tri"], _ffi.i32p) if d else None,
+                                         ptr(d["voxel"], _ffi.u32p) if d else None, C.byref(rays)),
+              "vrt_render_secondary")
+        return (vis, rays.value, d) if ids else (vis, rays.value)
+
+    def render_secondary_device(self, cam, film, spp, rank, nranks, d_prim_ptr, d_vis_ptr, stream_ptr=None):
+        check(lib().vrt_render_secondary_device(self.h, C.byref(cam.c), C.byref(film.c), int(spp), int(rank),
+                                                int(nranks), C.c_void_p(d_prim_ptr), C.c_void_p(d_vis_ptr),
+                                                C.c_void_p(stream_ptr) if stream_ptr else None),
+              "vrt_render_secondary_device")
+
     def render_tiles_device(self, cam, film, rank, nranks, image_layout, d_out_ptr, stream_ptr=None):
         check(lib().vrt_render_tiles_device(self.h, C.byref(cam.c), C.byref(film.c), int(rank),
                                             int(nranks), int(image_layout), C.c_void_p(d_out_ptr),

@@ -947,6 +947,104 @@ extern "C" int vrt_render(vrt_scene *s, const vrt_camera *cam,
         return VRT_OK;
 }
 
+// Res = *min_element(root.aabb.size() / powf(2, max_depth)) (VRT/main.cc:69-70)
+static float scene_res(const vrt_scene *s)
+{
+        const float p2 = std::pow(2.f, (float)s->max_depth);
+        float res = 0.f;
+        for (int k = 0; k < 3; ++k) {
+                const float v = (s->info.root_max[k] - s->info.root_min[k]) / p2;
+                if (k == 0 || v < res)
+                        res = v;
+        }
+        return res;
+}
+
+extern "C" int vrt_render_secondary_device(vrt_scene *s, const vrt_camera *cam,
+                                           const vrt_film *film, int spp,
+                                           int rank, int nranks, float *d_prim,
+                                           float *d_vis, void *stream)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !cam || !d_prim || !d_vis || spp < 1 || spp > 64)
+                return fail(VRT_E_INVALID, "bad argument (spp must be 1..64)");
+        if (int rc = film_ok(film))
+                return rc;
+        if (nranks < 1 || rank < 0 || rank >= nranks)
+                return fail(VRT_E_INVALID, "rank %d of %d", rank, nranks);
+        HIPCHK(hipSetDevice(s->device));
+        RenderParams p;
+        fill_render_params(s, cam, film, 0, 1, &p);
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        HIPCHK(hipEventRecord(s->ev0, st));
+        HIPCHK(launch_secondary(p, spp, rank, nranks, scene_res(s), d_prim, d_vis, nullptr, nullptr,
+                                nullptr, st));
+        HIPCHK(hipEventRecord(s->ev1, st));
+        s->timed = true;
+        return VRT_OK;
+}
+
+extern "C" int vrt_render_secondary(vrt_scene *s, const vrt_camera *cam,
+                                    const vrt_film *film, int spp, float *vis,
+                                    int32_t *s_hit, int32_t *s_tri,
+                                    uint32_t *s_vox, int64_t *rays)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !cam || !vis || spp < 1 || spp > 64)
+                return fail(VRT_E_INVALID, "bad argument (spp must be 1..64)");
+        if (int rc = film_ok(film))
+                return rc;
+        std::lock_guard<std::mutex> lk(s->mu);
+        HIPCHK(hipSetDevice(s->device));
+        const size_t npix = (size_t)film->nx * film->ny;
+        const size_t ns = npix * (size_t)spp;
+        const size_t narea = (size_t)(8 * (film->nx / 8)) * (8 * (film->ny / 8));
+        DevBuf dvis, dprim, dh, dt, dv;
+        HIPCHK(hipMalloc(&dvis.p, npix * 4));
+        HIPCHK(hipMemsetAsync(dvis.p, 0, npix * 4, s->stream));
+        HIPCHK(hipMalloc(&dprim.p, std::max<size_t>(1, narea) * 32));
+        if (s_hit) {
+                HIPCHK(hipMalloc(&dh.p, ns * 4));
+                HIPCHK(hipMemsetAsync(dh.p, 0, ns * 4, s->stream));
+        }
+        if (s_tri) {
+                HIPCHK(hipMalloc(&dt.p, ns * 4));
+                HIPCHK(hipMemsetAsync(dt.p, 0xFF, ns * 4, s->stream));
+        }
+        if (s_vox) {
+                HIPCHK(hipMalloc(&dv.p, ns * 4));
+                HIPCHK(hipMemsetAsync(dv.p, 0xFF, ns * 4, s->stream));
+        }
+        RenderParams p;
+        fill_render_params(s, cam, film, 0, 1, &p);
+        HIPCHK(hipEventRecord(s->ev0, s->stream));
+        HIPCHK(launch_secondary(p, spp, 0, 1, scene_res(s), static_cast<float *>(dprim.p),
+                                static_cast<float *>(dvis.p), static_cast<int32_t *>(dh.p),
+                                static_cast<int32_t *>(dt.p), static_cast<uint32_t *>(dv.p), s->stream));
+        HIPCHK(hipEventRecord(s->ev1, s->stream));
+        s->timed = true;
+        HIPCHK(hipStreamSynchronize(s->stream));
+        HIPCHK(hipMemcpy(vis, dvis.p, npix * 4, hipMemcpyDeviceToHost));
+        if (s_hit)
+                HIPCHK(hipMemcpy(s_hit, dh.p, ns * 4, hipMemcpyDeviceToHost));
+        if (s_tri)
+                HIPCHK(hipMemcpy(s_tri, dt.p, ns * 4, hipMemcpyDeviceToHost));
+        if (s_vox)
+                HIPCHK(hipMemcpy(s_vox, dv.p, ns * 4, hipMemcpyDeviceToHost));
+        if (rays) {
+                std::vector<float> prim(narea * 8);
+                if (narea)
+                        HIPCHK(hipMemcpy(prim.data(), dprim.p, narea * 32, hipMemcpyDeviceToHost));
+                int64_t hits = 0;
+                for (size_t i = 0; i < narea; ++i)
+                        hits += prim[8 * i] != 0.f;
+                *rays = (int64_t)narea + hits * spp;
+        }
+        return VRT_OK;
+}
+
 extern "C" int vrt_ray_march_batch_device(vrt_scene *s, const vrt_ray *d_rays,
                                           int64_t n, vrt_hit *d_hits,
                                           void *stream)

@@ -108,6 +108,10 @@ hipError_t launch_ray_march(const DevScene &sc, const void *d_rays,
 hipError_t launch_unpack(int nx, int ny, int ntx, int nty, int nranks,
                          int tiles_per_rank, const float *src, float *dst,
                          hipStream_t st);
+hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,
+                            int nranks, float res, float *prim, float *vis,
+                            int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox,
+                            hipStream_t st);
 hipError_t launch_selftest(const double *mt_in, double *mt_out,
                            const float *sat_in, int32_t *sat_out, int64_t n,
                            hipStream_t st);

@@ -632,7 +632,7 @@ template <bool kCount>
 // the unconstrained 4 waves/SIMD (99 VGPRs): the march is latency-bound.
 #define VRT_WAVES_PER_EU 6
 #endif
-__global__ __launch_bounds__(kBlock, VRT_WAVES_PER_EU) void k_render(RenderParams p)
+__global__ __launch_bounds__(kBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k_render(RenderParams p)
 {
         __shared__ uint32_t stk_base[kStack * kBlock];
         __shared__ uint32_t stk_ord[kStack * kBlock];
@@ -766,6 +766,197 @@ __global__ __launch_bounds__(kBlock) void k_ray_march(DevScene sc,
                 for (int q = 3; q < 9; ++q)
                         o[q] = 0;
         }
+}
+
+// ---------------------------------------------------------------------------
+// Config 5: one primary hit per pixel, then `spp` stochastic
+// secondary rays Ray{hit, normal + random_point_in_unit_sphere(pcg), res}.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kPcgMul = 6364136223846793005ULL;
+constexpr uint64_t kPcgInc = 1442695040888963407ULL;
+
+// jql::PCG::operator() (VRT/graphics_math.h:836-849)
+__device__ __forceinline__ uint32_t pcg_next(uint64_t &s)
+{
+        s = s * kPcgMul + kPcgInc;
+        const uint32_t xorshift = (uint32_t)((s ^ (s >> 18u)) >> 27u);
+        const uint32_t shift = (uint32_t)(s >> 59u);
+        return (xorshift >> shift) | (xorshift << ((0u - shift) & 31u));
+}
+
+// libstdc++ 11 uniform_real_distribution<float>{-1,1}: generate_canonical
+// <float,24> = float(g) / 2^32 (clamped below 1), then u * 2 + -1.
+__device__ __forceinline__ float uniform_m11(uint64_t &s)
+{
+        float sum = 0.0f;
+        sum += (float)pcg_next(s) * 1.0f;
+        float ret = sum / 4294967296.0f;
+        if (ret >= 1.0f)
+                ret = 0.99999994f;  // nextafter(1.f, 0.f)
+        return (ret * (1.0f - -1.0f)) + -1.0f;
+}
+
+// State after n more LCG steps (O(log n) jump-ahead, mod 2^64).
+__device__ __forceinline__ uint64_t pcg_advance(uint64_t s, uint64_t n)
+{
+        uint64_t am = 1, ap = 0, cm = kPcgMul, cp = kPcgInc;
+        while (n) {
+                if (n & 1) {
+                        am *= cm;
+                        ap = ap * cm + cp;
+                }
+                cp = (cm + 1) * cp;
+                cm *= cm;
+                n >>= 1;
+        }
+        return am * s + ap;
+}
+
+// Pass 1: pixel-centre primary ray (Camera::gen_rays1, VRT/camera.cc:77-93)
+// over the 8*(n/8) render area, one pixel per lane -> {hit, hit xyz, normal}.
+__global__ __launch_bounds__(kBlock) void k_primary1(RenderParams p, float *__restrict__ prim)
+{
+        __shared__ uint32_t stk_base[kStack * kBlock];
+        __shared__ uint32_t stk_ord[kStack * kBlock];
+        const int tid = threadIdx.x;
+        const int W8 = 8 * p.ntx, H8 = 8 * p.nty;
+        const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
+        if (i >= (int64_t)W8 * H8)
+                return;
+        const int px = (int)(i % W8), py = (int)(i / W8);
+        const CamParams &c = p.cam;
+        const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py, 0.5f, 0.5f);
+        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]), dn, c.tmin, c.tmax);
+        MarchResult m;
+        ray_march_dispatch<false>(p.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        float *o = prim + 8 * i;
+        if (!m.hit) {
+                o[0] = 0.f;
+                return;
+        }
+        const TriAttr *ta = p.sc.tri_attr + m.tri;
+        const f3 n0 = mk3(ta->n[0], ta->n[1], ta->n[2]);
+        const f3 n1 = mk3(ta->n[3], ta->n[4], ta->n[5]);
+        const f3 n2 = mk3(ta->n[6], ta->n[7], ta->n[8]);
+        const float w = clampf(1.0f - m.u - m.v, 0, 1);
+        const f3 nrm = normalize((n0 * w + n1 * m.u) + n2 * m.v);
+        o[0] = 1.f;
+        o[1] = m.hp.x;
+        o[2] = m.hp.y;
+        o[3] = m.hp.z;
+        o[4] = nrm.x;
+        o[5] = nrm.y;
+        o[6] = nrm.z;
+}
+
+// Pass 2: one wave per pixel, lane s = secondary ray s.  The reference
+// draws points sequentially (rejection sampling, 3 draws per attempt); here
+// lane l evaluates attempt l (+64 per round) from a jump-ahead PCG state and
+// the accepted attempts are ranked in attempt order with a ballot, so ray s
+// gets exactly the reference's s-th accepted point.
+struct SecondaryParams {
+        DevScene sc;
+        int32_t nx, W8, H8, spp;
+        int32_t rank, nranks;  // pixel p handled when (p / 64) % nranks == rank
+        float res;
+        const float *prim;
+        float *vis;            // nx*ny, this rank's pixels written
+        int32_t *s_hit, *s_tri;
+        uint32_t *s_vox;
+};
+
+__global__ __launch_bounds__(kBlock) void k_secondary(SecondaryParams p)
+{
+        __shared__ uint32_t stk_base[kStack * kBlock];
+        __shared__ uint32_t stk_ord[kStack * kBlock];
+        __shared__ float pts[4][64][3];
+        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        const int64_t npix = (int64_t)p.W8 * p.H8;
+        // this rank's k-th pixel: chunks of 64 pixels dealt round-robin
+        const int64_t k = (int64_t)blockIdx.x * 4 + wave;
+        const int64_t chunk = k >> 6;
+        const int64_t pix = ((chunk * p.nranks + p.rank) << 6) + (k & 63);
+        if (pix >= npix)
+                return;
+        const int px = (int)(pix % p.W8), py = (int)(pix / p.W8);
+        const float *pr = p.prim + 8 * pix;
+        const size_t vi = (size_t)py * p.nx + px;
+        if (pr[0] == 0.f) {  // primary miss: the wave leaves together
+                if (lane == 0)
+                        p.vis[vi] = 1.0f;
+                return;
+        }
+        const f3 hp = mk3(pr[1], pr[2], pr[3]);
+        const f3 nrm = mk3(pr[4], pr[5], pr[6]);
+        const uint64_t seed = 0xc01dbeefULL ^ (uint64_t)((uint64_t)py * (uint64_t)p.nx + (uint64_t)px);
+        uint64_t st = pcg_advance(seed, 3 * (uint64_t)lane);
+        int have = 0;
+        while (have < p.spp) {  // wave-uniform
+                uint64_t s2 = st;
+                const float x = uniform_m11(s2);
+                const float y = uniform_m11(s2);
+                const float z = uniform_m11(s2);
+                const bool acc = length(mk3(x, y, z)) < 1.f;
+                const uint64_t mask = __ballot(acc);
+                const int rk = have + (int)__popcll(mask & ((1ull << lane) - 1ull));
+                if (acc && rk < p.spp) {
+                        pts[wave][rk][0] = x;
+                        pts[wave][rk][1] = y;
+                        pts[wave][rk][2] = z;
+                }
+                have += (int)__popcll(mask);
+                st = pcg_advance(st, 192);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        bool hit = false;
+        if (lane < p.spp) {
+                const f3 pt = mk3(pts[wave][lane][0], pts[wave][lane][1], pts[wave][lane][2]);
+                const f3 dn = normalize(nrm + pt);  // Ray{hit, n + p, res} normalises d
+                const RayK r = make_rayk(hp, dn, p.res, kFltMax);
+                MarchResult m;
+                ray_march_dispatch<false>(p.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+                hit = m.hit;
+                const size_t si = vi * (size_t)p.spp + lane;
+                if (p.s_hit) p.s_hit[si] = m.hit ? 1 : 0;
+                if (p.s_tri) p.s_tri[si] = m.hit ? (int32_t)m.tri : -1;
+                if (p.s_vox) p.s_vox[si] = m.hit ? p.sc.node_vox[m.node] : 0xFFFFFFFFu;
+        }
+        const uint64_t hm = __ballot(hit);
+        if (lane == 0)
+                p.vis[vi] = (float)(p.spp - (int)__popcll(hm)) / (float)p.spp;
+}
+
+hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nranks, float res,
+                            float *prim, float *vis, int32_t *s_hit, int32_t *s_tri,
+                            uint32_t *s_vox, hipStream_t st)
+{
+        const int64_t npix = (int64_t)rp.ntx * 8 * rp.nty * 8;
+        if (npix <= 0)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_primary1, dim3((unsigned)((npix + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                           rp, prim);
+        SecondaryParams sp;
+        sp.sc = rp.sc;
+        sp.nx = rp.cam.nx;
+        sp.W8 = rp.ntx * 8;
+        sp.H8 = rp.nty * 8;
+        sp.spp = spp;
+        sp.rank = rank;
+        sp.nranks = nranks;
+        sp.res = res;
+        sp.prim = prim;
+        sp.vis = vis;
+        sp.s_hit = s_hit;
+        sp.s_tri = s_tri;
+        sp.s_vox = s_vox;
+        // pixels of this rank: whole 64-pixel chunks dealt round-robin
+        const int64_t chunks = (npix + 63) / 64;
+        const int64_t mine = (chunks - rank + nranks - 1) / nranks;
+        const int64_t waves = mine * 64;
+        hipLaunchKernelGGL(k_secondary, dim3((unsigned)((waves + 3) / 4)), dim3(kBlock), 0, st, sp);
+        return hipGetLastError();
 }
 
 // Rank-0 re-assembly of gathered per-rank tile buffers into the image.
