@@ -16,8 +16,9 @@ HIPFLAGS := -x hip --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 $(FP) -Iinclude -
             -Wall -Wno-unused-function -fvisibility=hidden
 CXXFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Wall -fvisibility=hidden
 
-OBJS := $(BLD)/vrt_kernels.o $(BLD)/vrt_host.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o
-HDRS := include/vrt.h $(SRC)/vrt_math.h $(SRC)/vrt_internal.h
+HOSTOBJS := $(BLD)/vrt_host.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o
+OBJS := $(BLD)/vrt_kernels.o $(HOSTOBJS)
+HDRS := include/vrt.h $(SRC)/vrt_math.h $(SRC)/vrt_internal.h $(SRC)/vrt_error.h
 
 all: $(PKG)/libvrt.so oracle
 
@@ -36,6 +37,12 @@ $(BLD)/vrt_hdr.o: $(SRC)/vrt_hdr.cpp include/vrt.h | $(BLD)
 $(BLD)/vrt_proxy.o: $(SRC)/vrt_proxy.cpp include/vrt.h | $(BLD)
 	g++ $(CXXFLAGS) -c $< -o $@
 
+$(BLD)/vrt_obj.o: $(SRC)/vrt_obj.cpp include/vrt.h $(SRC)/vrt_error.h | $(BLD)
+	g++ $(CXXFLAGS) -c $< -o $@
+
+$(BLD)/vrt_tga.o: $(SRC)/vrt_tga.cpp include/vrt.h $(SRC)/vrt_error.h | $(BLD)
+	g++ $(CXXFLAGS) -c $< -o $@
+
 $(PKG)/libvrt.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread
 
@@ -43,11 +50,11 @@ oracle:
 	$(MAKE) -C oracle
 
 # A/B variant of the kernels:  make variant NAME=v0 DEFS="-DVRT_EXPAND_V=0"
-variant: $(BLD)/vrt_host.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o | $(BLD)
+variant: $(HOSTOBJS) | $(BLD)
 	mkdir -p build/variants
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
-	  build/variants/k_$(NAME).o $(BLD)/vrt_host.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o -lpthread
+	  build/variants/k_$(NAME).o $(HOSTOBJS) -lpthread
 
 # ISA listing + register/occupancy report of the kernels (for DESIGN.md)
 isa: | $(BLD)

@@ -23,7 +23,7 @@ extern "C" {
 #define VRT_E_NOMEM (-2)    /* host allocation failed */
 #define VRT_E_DEVICE (-3)   /* HIP runtime error (see vrt_last_error) */
 #define VRT_E_NODEVICE (-4) /* no usable gfx950 device */
-#define VRT_E_IO (-5)       /* file could not be written */
+#define VRT_E_IO (-5)       /* file could not be opened / written */
 
 #define VRT_MAX_DEPTH 11    /* voxel ids pack 10 bits per axis */
 
@@ -224,6 +224,58 @@ int intersect_triangle3(double orig[3], double dir[3], double vert0[3],
 /* VRT/tribox2.h:6 */
 int triBoxOverlap(float boxcenter[3], float boxhalfsize[3],
                   float triverts[3][3]);
+
+/* ---- scene ingest (VRT/voxel_octree.cc:305-388) -------------------------
+ * vrt_obj_load = obj2voxel(path) + load_image for every texture a face
+ * uses: tinyobjloader v1.4.0 LoadObj(.., path, mtldir = dir(path) + "/",
+ * triangulate = true) restated bit-exactly (its non-correctly-rounded float
+ * parser and ear-clipping triangulation included), then one triangle per
+ * (shape, face) in shape order.  Textures are decoded like stbi_load(path,
+ * .., 0) (TGA only).  Faces without normals or with out-of-range indices
+ * are errors; faces without a material get an extra default material (Kd
+ * 0) appended after the file's materials.  VRT_OBJ_PARSE_ONLY stops after
+ * LoadObj (no soup, no textures; no normal requirement). */
+#define VRT_OBJ_PARSE_ONLY 1
+
+typedef struct vrt_obj vrt_obj;
+typedef struct {
+        int64_t nvert, nnormal, ntexcoord; /* attrib_t sizes / 3, / 3, / 2 */
+        int32_t nshape;                    /* shapes.size() */
+        int64_t nface;                     /* triangles over all shapes */
+        int32_t nmat;                      /* materials.size() (MTL order) */
+        int32_t has_soup;                  /* 0 with VRT_OBJ_PARSE_ONLY */
+        int32_t nsoup_mat;                 /* nmat (+1 if a default was added) */
+        int32_t ntex;
+        int64_t tex_bytes;
+} vrt_obj_info_t;
+
+int vrt_obj_load(const char *obj_path, int flags, vrt_obj **out);
+void vrt_obj_free(vrt_obj *o);
+int vrt_obj_info(const vrt_obj *o, vrt_obj_info_t *info);
+/* Borrowed views, valid until vrt_obj_free: attrib_t::vertices / normals /
+ * texcoords. */
+int vrt_obj_attrib(const vrt_obj *o, const float **v, const float **vn,
+                   const float **vt);
+/* Per triangle (shape order): idx[9] = {v, vn, vt} x 3 (0-based, -1 =
+ * absent), tinyobj material id (-1 = none) and shape index.  Any output may
+ * be NULL; sizes from vrt_obj_info().nface. */
+int vrt_obj_faces(const vrt_obj *o, int32_t *idx, int32_t *mat,
+                  int32_t *shape);
+/* material_t i: name, diffuse (Kd), diffuse_texname (as in the MTL). */
+int vrt_obj_material(const vrt_obj *o, int i, const char **name, float kd[3],
+                     const char **texname);
+/* Resolved file of soup texture i (mtldir + diffuse_texname). */
+int vrt_obj_texture_path(const vrt_obj *o, int i, const char **path);
+const char *vrt_obj_warnings(const vrt_obj *o);
+/* The soup as a scene descriptor for vrt_scene_create (borrowed pointers). */
+int vrt_obj_scene_desc(const vrt_obj *o, vrt_scene_desc *desc);
+
+/* stbi_load(path, &w, &h, &comp, 0) for TGA files (VRT/stb_image.h:
+ * 5404-5640): 8-bit interleaved, row 0 = top; free with vrt_image_free. */
+int vrt_tga_load(const char *path, int *w, int *h, int *comp, uint8_t **out);
+int vrt_tga_decode(const uint8_t *buf, int64_t len, int *w, int *h, int *comp,
+                   uint8_t **out);
+void vrt_image_free(uint8_t *p);
 
 /* ---- synthetic inputs ----------------------------------------------------
  * Deterministic "sponza-proxy" atrium (no Sponza asset ships): floor, walls,

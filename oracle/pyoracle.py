@@ -87,8 +87,77 @@ def reference():
         L.ref_tri_box_overlap.argtypes = [f32p, f32p, f32p]
         L.ref_write_hdr_mem.restype = C.c_long
         L.ref_write_hdr_mem.argtypes = [C.c_int, C.c_int, C.c_int, f32p, u8p, C.c_long]
+        L.ref_load_obj.restype = C.POINTER(_RefObj)
+        L.ref_load_obj.argtypes = [C.c_char_p, C.c_char_p]
+        L.ref_free_obj.restype = None
+        L.ref_free_obj.argtypes = [C.POINTER(_RefObj)]
+        L.ref_stbi_load.restype = u8p
+        L.ref_stbi_load.argtypes = [C.c_char_p, i32p, i32p, i32p]
+        L.ref_stbi_load_mem.restype = u8p
+        L.ref_stbi_load_mem.argtypes = [u8p, C.c_int, i32p, i32p, i32p]
+        L.ref_stbi_free.restype = None
+        L.ref_stbi_free.argtypes = [u8p]
+        L.ref_stbi_failure.restype = C.c_char_p
         _r = L
     return _r
+
+
+class _RefObj(C.Structure):
+    _fields_ = [("ok", C.c_int32), ("nv", C.c_int64), ("nvn", C.c_int64), ("nvt", C.c_int64),
+                ("v", f32p), ("vn", f32p), ("vt", f32p), ("nshape", C.c_int32), ("nface", C.c_int64),
+                ("fv", i32p), ("idx", i32p), ("mat", i32p), ("shape", i32p), ("nmat", C.c_int32),
+                ("kd", f32p), ("name", C.POINTER(C.c_char_p)), ("tex", C.POINTER(C.c_char_p)),
+                ("warn", C.c_char_p), ("err", C.c_char_p)]
+
+
+def ref_load_obj(path, mtl_basedir):
+    """tinyobj::LoadObj(.., path, mtl_basedir, triangulate=true) of the
+    reference (compiled in place), flattened to numpy."""
+    L = reference()
+    q = L.ref_load_obj(str(path).encode(), None if mtl_basedir is None else str(mtl_basedir).encode())
+    o = q.contents
+    try:
+        def arr(p, n, dt):
+            return np.ctypeslib.as_array(p, (n,)).astype(dt) if n else np.zeros(0, dt)
+        out = {"ok": bool(o.ok), "v": arr(o.v, o.nv * 3, np.float32).reshape(-1, 3),
+               "vn": arr(o.vn, o.nvn * 3, np.float32).reshape(-1, 3),
+               "vt": arr(o.vt, o.nvt * 2, np.float32).reshape(-1, 2), "nshape": o.nshape,
+               "fv": arr(o.fv, o.nface, np.int32), "idx": arr(o.idx, o.nface * 9, np.int32).reshape(-1, 3, 3),
+               "mat": arr(o.mat, o.nface, np.int32), "shape": arr(o.shape, o.nface, np.int32),
+               "kd": arr(o.kd, o.nmat * 3, np.float32).reshape(-1, 3),
+               "names": [o.name[i].decode(errors="surrogateescape") for i in range(o.nmat)],
+               "texnames": [o.tex[i].decode(errors="surrogateescape") for i in range(o.nmat)],
+               "warn": o.warn.decode(errors="replace"), "err": o.err.decode(errors="replace")}
+    finally:
+        L.ref_free_obj(q)
+    return out
+
+
+def _stbi_out(L, p, w, h, c):
+    if not p:
+        return None, L.ref_stbi_failure().decode()
+    try:
+        a = np.ctypeslib.as_array(p, (w.value * h.value * c.value,)).copy()
+    finally:
+        L.ref_stbi_free(p)
+    return a.reshape(h.value, w.value, c.value), ""
+
+
+def ref_stbi_load(path):
+    """stbi_load(path, &w, &h, &c, 0) -> (uint8 (h, w, c) or None, failure reason)."""
+    L = reference()
+    w, h, c = C.c_int(), C.c_int(), C.c_int()
+    p = L.ref_stbi_load(str(path).encode(), C.byref(w), C.byref(h), C.byref(c))
+    return _stbi_out(L, p, w, h, c)
+
+
+def ref_stbi_load_mem(data):
+    L = reference()
+    buf = np.frombuffer(bytes(data), np.uint8).copy()
+    w, h, c = C.c_int(), C.c_int(), C.c_int()
+    p = L.ref_stbi_load_mem(_p(buf, u8p) if buf.size else (C.c_uint8 * 1)(), buf.size, C.byref(w), C.byref(h),
+                            C.byref(c))
+    return _stbi_out(L, p, w, h, c)
 
 
 # ---------------------------------------------------------------- primitives

@@ -1,7 +1,8 @@
 """Regenerate the committed golden fixtures (run in the dev container, where
 /root/reference exists):
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py          # everything
+    python tests/golden/make_golden.py ingest   # ingest_ref.npz only
 
 * kat_raytri.npz / kat_tribox.npz / hdr_ref.npz -- outputs of the
   REFERENCE's own raytri.cc, tribox2.cc and stb_image_write.h, compiled
@@ -10,6 +11,9 @@
   restatement (oracle/vrt_oracle.c): hit, triangle id, voxel id, per-sample
   RGB, reference-equivalent counters and the accumulated image.  The oracle's
   floating-point leaves are pinned by the KATs above; see DESIGN.md.
+* ingest_ref.npz -- tinyobj::LoadObj and stbi_load outputs of the
+  REFERENCE (tiny_obj_loader.cc / stb_image.h compiled unmodified into
+  oracle/_ref/libvrtref.so) on the tests/ingest_corpus.py inputs.
 Only inputs and outputs are stored -- no reference source.
 """
 import os
@@ -169,9 +173,44 @@ def secondary_fixture(sd, depth, cam, film, spp, name):
     np.savez_compressed(os.path.join(HERE, f"secondary_{name}.npz"), **rec)
 
 
+def ingest_fixture():
+    """tinyobj::LoadObj (reference, compiled in place) on the deterministic
+    OBJ/MTL corpus of tests/ingest_corpus.py, and stbi_load_from_memory on
+    its TGA corpus.  Inputs are regenerated by the tests; their SHA-256 is
+    stored so a drifting generator cannot silently change the cases."""
+    import hashlib
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ingest_corpus as ic
+    rec = {}
+    with tempfile.TemporaryDirectory() as td:
+        cases = ic.write_obj_corpus(td)
+        for name, (fn, _parse_only) in sorted(cases.items()):
+            path = os.path.join(td, fn)
+            rec[f"{name}_sha"] = np.array(hashlib.sha256(open(path, "rb").read()).hexdigest())
+            r = po.ref_load_obj(path, td + "/")
+            assert r["ok"], (name, r["err"])
+            for k in ("v", "vn", "vt", "idx", "mat", "shape", "kd"):
+                rec[f"{name}_{k}"] = r[k]
+            rec[f"{name}_nshape"] = np.int32(r["nshape"])
+            rec[f"{name}_names"] = np.array(r["names"], dtype=str)
+            rec[f"{name}_texnames"] = np.array(r["texnames"], dtype=str)
+    for name, data in ic.tga_corpus():
+        img, _why = po.ref_stbi_load_mem(data)
+        rec[f"tga_{name}_sha"] = np.array(hashlib.sha256(data).hexdigest())
+        rec[f"tga_{name}_ok"] = np.int32(img is not None)
+        if img is not None:
+            rec[f"tga_{name}_img"] = img
+    np.savez_compressed(os.path.join(HERE, "ingest_ref.npz"), **rec)
+
+
 def main():
     if not po.reference_available():
         raise SystemExit("oracle/_ref/libvrtref.so missing: run `make` where /root/reference exists")
+    if sys.argv[1:] == ["ingest"]:
+        ingest_fixture()
+        return
+    ingest_fixture()
     q, out = kat_raytri()
     np.savez_compressed(os.path.join(HERE, "kat_raytri.npz"), inp=q, out=out)
     q, out = kat_tribox()

@@ -7,15 +7,16 @@ the library and raises if it is missing: there is no CPU fallback.
 """
 from ._ffi import VrtError, lib, LIB_PATH  # noqa: F401
 from .api import (  # noqa: F401
-    FLT_MAX, Camera, Film, SceneData, VoxelOctree, device_count, device_selftest,
-    hdr_bytes, intersect_triangle3, make_ray, ray_march, ray_march_init, render,
-    sweep_pose, tiles_per_rank, to_radian, tri_box_overlap, unpack_tiles_device,
-    write_hdr,
+    FLT_MAX, Camera, Film, ObjModel, SceneData, VoxelOctree, device_count, device_selftest,
+    hdr_bytes, intersect_triangle3, load_image, make_ray, obj2voxel, ray_march, ray_march_init,
+    render, sweep_pose, tga_decode, tiles_per_rank, to_radian, tri_box_overlap,
+    unpack_tiles_device, write_hdr,
 )
 
 __all__ = [
     "VrtError", "lib", "LIB_PATH", "FLT_MAX", "Camera", "Film", "SceneData", "VoxelOctree",
     "device_count", "device_selftest", "hdr_bytes", "intersect_triangle3", "make_ray",
     "ray_march", "ray_march_init", "render", "sweep_pose", "tiles_per_rank", "to_radian",
-    "tri_box_overlap", "unpack_tiles_device", "write_hdr",
+    "tri_box_overlap", "unpack_tiles_device", "write_hdr", "ObjModel", "obj2voxel", "load_image",
+    "tga_decode",
 ]

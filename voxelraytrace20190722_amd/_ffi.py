@@ -73,6 +73,15 @@ class Stats(C.Structure):
                 ("hits", C.c_uint64), ("kernel_ms", C.c_double)]
 
 
+class ObjInfo(C.Structure):
+    _fields_ = [("nvert", C.c_int64), ("nnormal", C.c_int64), ("ntexcoord", C.c_int64),
+                ("nshape", C.c_int32), ("nface", C.c_int64), ("nmat", C.c_int32),
+                ("has_soup", C.c_int32), ("nsoup_mat", C.c_int32), ("ntex", C.c_int32),
+                ("tex_bytes", C.c_int64)]
+
+
+VRT_OBJ_PARSE_ONLY = 1
+
 _P = C.c_void_p
 SIGNATURES = {
     "vrt_device_count": (C.c_int, [i32p]),
@@ -109,6 +118,18 @@ SIGNATURES = {
     "vrt_proxy_scene": (C.c_int, [C.c_double, C.c_uint32, i32p, f32p, f32p, f32p, i32p,
                                   i32p, i32p, f32p, i32p, i32p, i64p, u8p, i64p]),
     "vrt_sweep_pose": (C.c_int, [f32p, f32p, C.c_int, C.c_int, f32p, f32p, f32p, f32p]),
+    "vrt_obj_load": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_P)]),
+    "vrt_obj_free": (None, [_P]),
+    "vrt_obj_info": (C.c_int, [_P, C.POINTER(ObjInfo)]),
+    "vrt_obj_attrib": (C.c_int, [_P, C.POINTER(f32p), C.POINTER(f32p), C.POINTER(f32p)]),
+    "vrt_obj_faces": (C.c_int, [_P, i32p, i32p, i32p]),
+    "vrt_obj_material": (C.c_int, [_P, C.c_int, C.POINTER(C.c_char_p), f32p, C.POINTER(C.c_char_p)]),
+    "vrt_obj_texture_path": (C.c_int, [_P, C.c_int, C.POINTER(C.c_char_p)]),
+    "vrt_obj_warnings": (C.c_char_p, [_P]),
+    "vrt_obj_scene_desc": (C.c_int, [_P, C.POINTER(SceneDesc)]),
+    "vrt_tga_load": (C.c_int, [C.c_char_p, i32p, i32p, i32p, C.POINTER(u8p)]),
+    "vrt_tga_decode": (C.c_int, [u8p, C.c_int64, i32p, i32p, i32p, C.POINTER(u8p)]),
+    "vrt_image_free": (None, [u8p]),
     "vrt_status_string": (C.c_char_p, [C.c_int]),
     "vrt_last_error": (C.c_char_p, []),
 }

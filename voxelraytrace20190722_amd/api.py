@@ -146,6 +146,132 @@ class SceneData:
                                 C.byref(tb)), "vrt_proxy_scene")
         return cls(pos, nrm, uv, mat, mt, kd, td, to, tx)
 
+    @classmethod
+    def from_obj(cls, path):
+        """obj2voxel(path) + textures (VRT/voxel_octree.cc:305-388)."""
+        with ObjModel(path) as m:
+            return m.scene_data()
+
+
+class ObjModel:
+    """tinyobj::LoadObj result (+ the obj2voxel soup unless parse_only)
+    through vrt_obj_load.  Usable as a context manager; arrays returned are
+    copies, so they outlive the handle."""
+
+    def __init__(self, path, parse_only=False):
+        self.h = C.c_void_p()
+        flags = _ffi.VRT_OBJ_PARSE_ONLY if parse_only else 0
+        check(lib().vrt_obj_load(str(path).encode(), flags, C.byref(self.h)), f"vrt_obj_load({path})")
+        self.info = _ffi.ObjInfo()
+        check(lib().vrt_obj_info(self.h, C.byref(self.info)), "vrt_obj_info")
+
+    def close(self):
+        if self.h:
+            lib().vrt_obj_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown: module globals already gone
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def attrib(self):
+        """(vertices (n,3), normals (n,3), texcoords (n,2)) float32."""
+        v, vn, vt = _ffi.f32p(), _ffi.f32p(), _ffi.f32p()
+        check(lib().vrt_obj_attrib(self.h, C.byref(v), C.byref(vn), C.byref(vt)), "vrt_obj_attrib")
+        i = self.info
+
+        def arr(p, n, k):
+            if n == 0:
+                return np.zeros((0, k), np.float32)
+            return np.ctypeslib.as_array(p, (n * k,)).reshape(n, k).copy()
+        return arr(v, i.nvert, 3), arr(vn, i.nnormal, 3), arr(vt, i.ntexcoord, 2)
+
+    def faces(self):
+        """Per triangle: idx (n,3,3) {v,vn,vt} per corner, material id, shape."""
+        n = self.info.nface
+        idx = np.zeros((n, 3, 3), np.int32)
+        mat = np.zeros(n, np.int32)
+        shp = np.zeros(n, np.int32)
+        check(lib().vrt_obj_faces(self.h, ptr(idx, _ffi.i32p), ptr(mat, _ffi.i32p), ptr(shp, _ffi.i32p)),
+              "vrt_obj_faces")
+        return idx, mat, shp
+
+    def materials(self):
+        out = []
+        for i in range(self.info.nmat):
+            name, tex = C.c_char_p(), C.c_char_p()
+            kd = np.zeros(3, np.float32)
+            check(lib().vrt_obj_material(self.h, i, C.byref(name), ptr(kd, _ffi.f32p), C.byref(tex)),
+                  "vrt_obj_material")
+            out.append({"name": name.value.decode(errors="surrogateescape"), "kd": kd,
+                        "texname": tex.value.decode(errors="surrogateescape")})
+        return out
+
+    def texture_paths(self):
+        out = []
+        for i in range(self.info.ntex):
+            p = C.c_char_p()
+            check(lib().vrt_obj_texture_path(self.h, i, C.byref(p)), "vrt_obj_texture_path")
+            out.append(p.value.decode(errors="surrogateescape"))
+        return out
+
+    def warnings(self):
+        return lib().vrt_obj_warnings(self.h).decode(errors="replace")
+
+    def scene_data(self):
+        d = _ffi.SceneDesc()
+        check(lib().vrt_obj_scene_desc(self.h, C.byref(d)), "vrt_obj_scene_desc")
+        n, nm, nt = d.ntri, d.nmat, d.ntex
+
+        def cp(p, count, dt):
+            if count == 0:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(p, (count,)).copy()
+        return SceneData(cp(d.pos, n * 9, np.float32), cp(d.nrm, n * 9, np.float32), cp(d.uv, n * 6, np.float32),
+                         cp(d.mat, n, np.int32), cp(d.mat_tex, nm, np.int32), cp(d.mat_kd, nm * 3, np.float32),
+                         cp(d.tex_dims, nt * 3, np.int32), cp(d.tex_off, nt, np.int64),
+                         cp(d.tex_data, d.tex_bytes, np.uint8))
+
+
+def obj2voxel(path):
+    """The reference's obj2voxel (VRT/voxel_octree.cc:305-371) as SceneData."""
+    return SceneData.from_obj(path)
+
+
+def _image_out(rc, where, w, h, c, p):
+    check(rc, where)
+    try:
+        n = w.value * h.value * c.value
+        a = np.ctypeslib.as_array(p, (n,)).copy()
+    finally:
+        lib().vrt_image_free(p)
+    return a.reshape(h.value, w.value, c.value)
+
+
+def load_image(path):
+    """stbi_load(path, .., 0) for TGA (VRT/voxel_octree.cc:373-388):
+    uint8 (h, w, channels), row 0 = top."""
+    w, h, c, p = C.c_int32(), C.c_int32(), C.c_int32(), _ffi.u8p()
+    rc = lib().vrt_tga_load(str(path).encode(), C.byref(w), C.byref(h), C.byref(c), C.byref(p))
+    return _image_out(rc, f"vrt_tga_load({path})", w, h, c, p)
+
+
+def tga_decode(data):
+    """stbi_load_from_memory for TGA bytes."""
+    buf = np.frombuffer(bytes(data), np.uint8)
+    w, h, c, p = C.c_int32(), C.c_int32(), C.c_int32(), _ffi.u8p()
+    rc = lib().vrt_tga_decode(ptr(buf, _ffi.u8p) if buf.size else (C.c_uint8 * 1)(), buf.size, C.byref(w),
+                              C.byref(h), C.byref(c), C.byref(p))
+    return _image_out(rc, "vrt_tga_decode", w, h, c, p)
+
 
 class VoxelOctree:
     """The octree built by gi::ray_march_init and resident on one device

@@ -9,6 +9,7 @@
 //
 // VRT/x = /root/reference/VoxelRayTrace20190722/x
 #include "../../include/vrt.h"
+#include "vrt_error.h"
 #include "vrt_internal.h"
 
 #include <algorithm>
@@ -31,14 +32,30 @@ using namespace vrt;
 // ---------------------------------------------------------------------------
 static thread_local std::string g_err;
 
-static int fail(int code, const char *fmt, ...)
+static int vfail(int code, const char *fmt, va_list ap)
 {
         char buf[512];
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        g_err = buf;
+        return code;
+}
+
+static int fail(int code, const char *fmt, ...)
+{
         va_list ap;
         va_start(ap, fmt);
-        vsnprintf(buf, sizeof buf, fmt, ap);
+        vfail(code, fmt, ap);
         va_end(ap);
-        g_err = buf;
+        return code;
+}
+
+// shared with the ingest sources (vrt_obj.cpp, vrt_tga.cpp); hidden symbol
+int vrt::set_error(int code, const char *fmt, ...)
+{
+        va_list ap;
+        va_start(ap, fmt);
+        vfail(code, fmt, ap);
+        va_end(ap);
         return code;
 }
 
