@@ -216,6 +216,17 @@ int vrt_write_hdr(const char *filename, int w, int h, int comp,
 int64_t vrt_write_hdr_mem(int w, int h, int comp, const float *data,
                           uint8_t *out, int64_t cap);
 
+/* Device half of the writer: stbiw__linear_to_rgbe for every pixel of a
+ * device image (w*h*comp floats) into w*h*4 device bytes on `stream`; then
+ * vrt_write_hdr_rgbe[_mem] RLE-encodes those bytes on the host.  The file is
+ * byte-identical to vrt_write_hdr / stbi_write_hdr on the same pixels. */
+int vrt_rgbe_device(const float *d_img, int w, int h, int comp,
+                    uint8_t *d_rgbe, void *stream);
+int vrt_write_hdr_rgbe(const char *filename, int w, int h,
+                       const uint8_t *rgbe);
+int64_t vrt_write_hdr_rgbe_mem(int w, int h, const uint8_t *rgbe,
+                               uint8_t *out, int64_t cap);
+
 /* ---- legacy reference symbols (identical signatures and results) ------- */
 /* VRT/raytri.h:5-7 */
 int intersect_triangle3(double orig[3], double dir[3], double vert0[3],

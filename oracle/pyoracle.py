@@ -200,6 +200,21 @@ def ref_hdr_bytes(img):
     return buf.tobytes()
 
 
+def linear_to_rgbe_img(img):
+    """stbiw__linear_to_rgbe per pixel of an (h, w, comp) float image ->
+    (h, w, 4) uint8 (comp 1/2: grey; comp >= 3: first three channels)."""
+    img = np.asarray(img, np.float32)
+    if img.ndim == 2:
+        img = img[:, :, None]
+    h, w, c = img.shape
+    lin = np.ascontiguousarray(np.repeat(img[:, :, :1], 3, 2) if c < 3 else img[:, :, :3]).reshape(-1, 3)
+    out = np.zeros((h * w, 4), np.uint8)
+    f = oracle().ora_linear_to_rgbe
+    for i in range(h * w):
+        f(_p(lin[i], f32p), _p(out[i], u8p))
+    return out.reshape(h, w, 4)
+
+
 def uniform_draws(seed, n):
     st = C.c_uint64(seed)
     return np.array([oracle().ora_uniform_m11(C.byref(st)) for _ in range(n)], np.float32)

@@ -348,3 +348,38 @@ def tga_corpus(seed=23):
                       ("empty", b""), ("short", b"\0\0\2")]:
         cases.append((name, hdr))
     return cases
+
+
+def write_scene_obj(d, sd, name="scene"):
+    """SceneData -> OBJ + MTL + TGA textures (one `v/vt/vn` corner per
+    triangle vertex, one usemtl run per material change): the way a user's
+    asset reaches obj2voxel.  Returns the OBJ path."""
+    os.makedirs(os.path.join(d, "textures"), exist_ok=True)
+    with open(os.path.join(d, f"{name}.mtl"), "w") as f:
+        for m in range(len(sd.mat_tex)):
+            f.write(f"newmtl m{m}\nKd {' '.join(_fmt(x) for x in sd.mat_kd[m])}\n")
+            t = int(sd.mat_tex[m])
+            if t >= 0:
+                f.write(f"map_Kd textures/t{t}.tga\n")
+    for t in range(len(sd.tex_off)):
+        w, h, c = (int(x) for x in sd.tex_dims[t])
+        px = sd.tex_data[sd.tex_off[t]: sd.tex_off[t] + w * h * c].reshape(h, w, c)
+        with open(os.path.join(d, "textures", f"t{t}.tga"), "wb") as f:
+            f.write(tga_encode(px, rle=bool(t % 2), bottom_up=True))
+    n = sd.ntri
+    uv = sd.uv if sd.uv is not None else np.zeros((n, 6), np.float32)
+    mat = sd.mat if sd.mat is not None else np.zeros(n, np.int32)
+    lines = [f"mtllib {name}.mtl", f"o {name}"]
+    lines += ["v " + " ".join(_fmt(x) for x in p) for p in sd.pos.reshape(-1, 3)]
+    lines += ["vn " + " ".join(_fmt(x) for x in p) for p in sd.nrm.reshape(-1, 3)]
+    lines += ["vt " + " ".join(_fmt(x) for x in p) for p in uv.reshape(-1, 2)]
+    cur = None
+    for i in range(n):
+        if mat[i] != cur:
+            cur = mat[i]
+            lines.append(f"usemtl m{cur}")
+        a = 3 * i + 1
+        lines.append(f"f {a}/{a}/{a} {a + 1}/{a + 1}/{a + 1} {a + 2}/{a + 2}/{a + 2}")
+    path = os.path.join(d, f"{name}.obj")
+    write_text(path, lines)
+    return path

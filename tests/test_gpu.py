@@ -247,3 +247,56 @@ def test_secondary_rank_partition_sums_to_image(proxy_small):
         torch.cuda.synchronize()
         acc += part
     assert np.array_equal(bits(acc.cpu().numpy()), bits(ref))
+
+
+def test_obj_ingest_render_matches_oracle(tmp_path):
+    """OBJ/MTL/TGA -> vrt_obj_load (tinyobj-exact) -> octree -> GPU render,
+    bit-exact against the oracle on the same ingested soup; the corpus soup
+    itself is pinned to the reference's LoadObj by tests/test_ingest.py."""
+    import ingest_corpus as ic
+    cases = ic.write_obj_corpus(str(tmp_path / "corpus"))
+    scenes = [vrt.obj2voxel(str(tmp_path / "corpus" / cases["polys"][0]))]
+    proxy = vrt.SceneData.proxy(0.05, 3)
+    scenes.append(vrt.obj2voxel(ic.write_scene_obj(str(tmp_path / "proxy"), proxy)))
+    assert scenes[1].ntri == proxy.ntri and len(scenes[1].tex_off) == len(proxy.tex_off)
+    for sd in scenes:
+        tree = vrt.VoxelOctree(sd, 7)
+        osc = po.Scene(sd, 7)
+        mn, mx = tree.root_box
+        for pose in (2, 9):
+            fov, eye, spot, up = vrt.sweep_pose(mn, mx, pose, 16)
+            rgb, so = tree.render(vrt.Camera(fov, eye, spot, up), vrt.Film(1, 1, 48, 40), samples=True)
+            orgb, oso = osc.render(po.camera(fov, eye, spot, up), 1.0, 1.0, 48, 40, film_index=1, nthreads=8)
+            for key in ("hit", "tri", "voxel"):
+                assert np.array_equal(so[key], oso[key]), key
+            assert np.array_equal(bits(rgb), bits(orgb))
+            assert so["hit"].mean() > 0.2
+
+
+def test_device_rgbe_pack_matches_reference_writer(tmp_path):
+    """k_rgbe (device stbiw__linear_to_rgbe) + host RLE == stbi_write_hdr:
+    reference fixture images, plus an edge image (NaN, +-inf, huge,
+    negative, below the 1e-32 cut, denormals, exact powers of two)."""
+    import torch
+    z = golden("hdr_ref.npz")
+    imgs = [z[f"img{i}"] for i in range(6)]
+    edge = np.random.default_rng(4).random((7, 33, 3)).astype(np.float32)
+    specials = [np.nan, np.inf, -np.inf, 3e38, -1.0, 1e-33, 1e-40, 0.5, 1.0, 2.0, 255.99, 1e-32, 1.0000001e-32]
+    for k, v in enumerate(specials):
+        edge[k % 7, (3 * k) % 33, k % 3] = v
+    edge[6, :, :] = np.float32(2.0) ** np.arange(-40, 59, 3)[:33, None].astype(np.float32)
+    imgs.append(edge)
+    for i, img in enumerate(imgs):
+        img = np.ascontiguousarray(img, np.float32)
+        h, w = img.shape[:2]
+        comp = 1 if img.ndim == 2 else img.shape[2]
+        d = torch.from_numpy(img.reshape(-1).copy()).cuda()
+        out = torch.zeros(h * w * 4, dtype=torch.uint8, device="cuda")
+        vrt.rgbe_device(d.data_ptr(), w, h, comp, out.data_ptr())
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().reshape(h, w, 4)
+        assert np.array_equal(got, po.linear_to_rgbe_img(img)), i
+        p = tmp_path / f"d{i}.hdr"
+        assert vrt.write_hdr_device(p, d.data_ptr(), w, h, comp)
+        want = z[f"bytes{i}"].tobytes() if i < 6 else vrt.hdr_bytes(img)
+        assert p.read_bytes() == want, i

@@ -169,6 +169,22 @@ def test_hdr_live_vs_reference(tmp_path):
     assert p.read_bytes() == po.ref_hdr_bytes(img)
 
 
+def test_hdr_from_packed_rgbe_matches_reference_fixture(tmp_path):
+    """The host RLE half of the device writer (vrt_write_hdr_rgbe): RGBE
+    bytes from the oracle's stbiw__linear_to_rgbe -> the reference's file."""
+    z = golden("hdr_ref.npz")
+    i = 0
+    while f"img{i}" in z:
+        rgbe = po.linear_to_rgbe_img(z[f"img{i}"])
+        assert vrt.hdr_bytes_from_rgbe(rgbe) == z[f"bytes{i}"].tobytes(), i
+        i += 1
+    rgbe = po.linear_to_rgbe_img(z["img1"])
+    p = tmp_path / "r.hdr"
+    assert vrt.lib().vrt_write_hdr_rgbe(str(p).encode(), rgbe.shape[1], rgbe.shape[0],
+                                        rgbe.ctypes.data_as(vrt._ffi.u8p)) == 1
+    assert p.read_bytes() == z["bytes1"].tobytes()
+
+
 def test_write_hdr_errors(tmp_path):
     assert not vrt.write_hdr(tmp_path / "nodir" / "x.hdr", np.zeros((2, 2, 3), np.float32))
 

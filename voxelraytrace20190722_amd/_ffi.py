@@ -113,6 +113,9 @@ SIGNATURES = {
     "vrt_device_selftest": (C.c_int, [C.c_int, f64p, f64p, f32p, i32p, C.c_int64]),
     "vrt_write_hdr": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, f32p]),
     "vrt_write_hdr_mem": (C.c_int64, [C.c_int, C.c_int, C.c_int, f32p, u8p, C.c_int64]),
+    "vrt_rgbe_device": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P]),
+    "vrt_write_hdr_rgbe": (C.c_int, [C.c_char_p, C.c_int, C.c_int, u8p]),
+    "vrt_write_hdr_rgbe_mem": (C.c_int64, [C.c_int, C.c_int, u8p, u8p, C.c_int64]),
     "intersect_triangle3": (C.c_int, [f64p, f64p, f64p, f64p, f64p, f64p, f64p, f64p]),
     "triBoxOverlap": (C.c_int, [f32p, f32p, f32p]),
     "vrt_proxy_scene": (C.c_int, [C.c_double, C.c_uint32, i32p, f32p, f32p, f32p, i32p,

@@ -448,6 +448,35 @@ def hdr_bytes(img):
     return buf.tobytes()
 
 
+def hdr_bytes_from_rgbe(rgbe):
+    """stbi_write_hdr bytes from packed RGBE (h, w, 4) uint8 (vrt_write_hdr_rgbe_mem)."""
+    rgbe = np.ascontiguousarray(np.asarray(rgbe, np.uint8))
+    h, w = rgbe.shape[:2]
+    n = lib().vrt_write_hdr_rgbe_mem(w, h, ptr(rgbe, _ffi.u8p), None, 0)
+    if n == 0:
+        raise VrtError(_ffi.VRT_E_INVALID, "vrt_write_hdr_rgbe_mem")
+    buf = np.zeros(-n, np.uint8)
+    assert lib().vrt_write_hdr_rgbe_mem(w, h, ptr(rgbe, _ffi.u8p), ptr(buf, _ffi.u8p), -n) == -n
+    return buf.tobytes()
+
+
+def rgbe_device(d_img_ptr, w, h, comp, d_rgbe_ptr, stream_ptr=None):
+    """k_rgbe: pack a device float image (w*h*comp) into w*h*4 RGBE bytes."""
+    check(lib().vrt_rgbe_device(C.c_void_p(d_img_ptr), int(w), int(h), int(comp), C.c_void_p(d_rgbe_ptr),
+                                None if stream_ptr is None else C.c_void_p(stream_ptr)), "vrt_rgbe_device")
+
+
+def write_hdr_device(path, d_img_ptr, w, h, comp=3, stream_ptr=None):
+    """stbi_write_hdr of a device-resident image: RGBE packed on the GPU,
+    4 bytes/pixel copied back, RLE on the host.  Byte-identical to write_hdr."""
+    import torch
+    rgbe = torch.empty(int(w) * int(h) * 4, dtype=torch.uint8, device="cuda")
+    rgbe_device(d_img_ptr, w, h, comp, rgbe.data_ptr(), stream_ptr)
+    torch.cuda.synchronize()
+    host = rgbe.cpu().numpy()
+    return lib().vrt_write_hdr_rgbe(str(path).encode(), int(w), int(h), ptr(host, _ffi.u8p)) == 1
+
+
 def write_hdr(path, img):
     """stbi_write_hdr(path, w, h, comp, data): True on success."""
     img = np.ascontiguousarray(np.asarray(img, np.float32))

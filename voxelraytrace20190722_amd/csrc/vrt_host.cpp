@@ -864,6 +864,14 @@ extern "C" int vrt_unpack_tiles_device(const vrt_film *film, int nranks,
         return VRT_OK;
 }
 
+extern "C" int vrt_rgbe_device(const float *d_img, int w, int h, int comp, uint8_t *d_rgbe, void *stream)
+{
+        if (!d_img || !d_rgbe || w <= 0 || h <= 0 || comp < 1 || comp > 4)
+                return fail(VRT_E_INVALID, "vrt_rgbe_device: bad argument");
+        HIPCHK(launch_rgbe(d_img, (int64_t)w * h, comp, d_rgbe, static_cast<hipStream_t>(stream)));
+        return VRT_OK;
+}
+
 namespace {
 struct DevBuf {
         void *p = nullptr;

@@ -112,6 +112,7 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,
                             int nranks, float res, float *prim, float *vis,
                             int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox,
                             hipStream_t st);
+hipError_t launch_rgbe(const float *img, int64_t npx, int comp, uint8_t *out, hipStream_t st);
 hipError_t launch_selftest(const double *mt_in, double *mt_out,
                            const float *sat_in, int32_t *sat_out, int64_t n,
                            hipStream_t st);

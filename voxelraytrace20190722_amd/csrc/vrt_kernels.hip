@@ -22,6 +22,8 @@
 // VRT/x = /root/reference/VoxelRayTrace20190722/x
 #include "vrt_internal.h"
 
+#include <climits>
+
 namespace vrt {
 
 constexpr int kBlock = 256;
@@ -1028,6 +1030,52 @@ hipError_t launch_ray_march(const DevScene &sc, const void *d_rays, int64_t n,
         hipLaunchKernelGGL(k_ray_march, dim3((unsigned)grid), dim3(kBlock), 0, st,
                            sc, static_cast<const float *>(d_rays), n,
                            static_cast<uint32_t *>(d_hits));
+        return hipGetLastError();
+}
+
+// stbiw__linear_to_rgbe (VRT/stb_image_write.h:601-616) per pixel, the
+// per-pixel half of stbi_write_hdr (the scanline RLE stays on the host,
+// vrt_hdr.cpp).  Byte-identical to the reference's x86-64 build:
+// frexp of the float max component (glibc: NaN / inf keep exponent 0),
+// nrm = (m * 256) / max with a correctly rounded divide, and
+// (unsigned char)(float) as cvttss2si (out of range / NaN -> INT_MIN).
+__device__ __forceinline__ unsigned char cvt_uchar(float f)
+{
+        const int i = (f >= -2147483648.0f && f < 2147483648.0f) ? (int)f : INT_MIN;
+        return (unsigned char)i;
+}
+
+__global__ void k_rgbe(const float *__restrict__ img, int64_t npx, int comp,
+                       uchar4 *__restrict__ out)
+{
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= npx)
+                return;
+        const float *q = img + i * comp;
+        const float r = q[0];
+        const float g = comp >= 3 ? q[1] : r;
+        const float b = comp >= 3 ? q[2] : r;
+        const float m12 = g > b ? g : b;
+        const float mx = r > m12 ? r : m12;
+        uchar4 o = make_uchar4(0, 0, 0, 0);
+        if (!(mx < 1e-32f)) {
+                int e = 0;
+                float m = mx;
+                if (__builtin_isfinite(mx))
+                        m = frexpf(mx, &e);
+                const float nrm = __fdiv_rn(m * 256.0f, mx);
+                o = make_uchar4(cvt_uchar(__fmul_rn(r, nrm)), cvt_uchar(__fmul_rn(g, nrm)),
+                                cvt_uchar(__fmul_rn(b, nrm)), (unsigned char)(e + 128));
+        }
+        out[i] = o;
+}
+
+hipError_t launch_rgbe(const float *img, int64_t npx, int comp, uint8_t *out, hipStream_t st)
+{
+        if (npx <= 0)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_rgbe, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, st, img, npx, comp,
+                           reinterpret_cast<uchar4 *>(out));
         return hipGetLastError();
 }
 
