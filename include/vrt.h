@@ -207,6 +207,43 @@ int vrt_ray_march_batch_device(vrt_scene *s, const vrt_ray *d_rays, int64_t n,
 int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
                         const float *sat_in, int32_t *sat_out, int64_t n);
 
+/* ---- full trace() (VRT/main.cc:10-30, 79-123) -------
+ * The reference's actual image: a light pass from a light camera
+ * (render_mt + gen_rays4; every hit adds clamp(dot(illum_d[i], n), 0, 1) *
+ * get_diffuse to leaf->illum[i]), cone_trace_init_filter, then per camera
+ * sample trace(root, ray, 5, true) = sky on a miss, else get_albedo *
+ * (6-cone cone_trace + leaf compute_illum(-d)), accumulated with
+ * Film::add(c * .25f).  The reference's light-map += races across threads;
+ * here the per-leaf sums run in the canonical single-threaded order (task
+ * t = tx*8+ty, pixels row-major, samples 0..3), so results are
+ * deterministic and bit-identical to the oracle's single-threaded order.
+ *
+ * vrt_lightmap_build: light pass + filter on the scene's device (blocking);
+ * hits (may be NULL) = light samples that hit.  A new build replaces the
+ * previous light map. */
+int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
+                       const vrt_film *light_film, int64_t *hits);
+/* Per node (vrt_scene_info().nodes entries, BFS order): key = depth << 32 |
+ * ix | iy<<10 | iz<<20 (coords at that depth), VoxelOctree::coverage and
+ * illum[6][3].  coverage / illum may be NULL. */
+int vrt_lightmap_nodes(vrt_scene *s, uint64_t *key, float *coverage,
+                       float *illum);
+/* min component of root.size() / powf(2, levels) -- the reference's Res
+ * (VRT/main.cc:69-70); levels <= 0 uses the scene's max_depth. */
+int vrt_scene_min_voxel(const vrt_scene *s, int levels, float *res);
+/* Cone-tracing render with min_voxel_size = min_voxel (<= 0: the scene's
+ * Res).  rgb: host nx*ny*3 (index y*nx+x); s_hit / s_rgb optional
+ * per-sample outputs ((py*nx+px)*4+s). */
+int vrt_render_trace(vrt_scene *s, const vrt_camera *cam, const vrt_film *film,
+                     float min_voxel, float *rgb, int32_t *s_hit,
+                     float *s_rgb);
+/* Device-resident variant with the tile partition of
+ * vrt_render_tiles_device. */
+int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam,
+                            const vrt_film *film, float min_voxel, int rank,
+                            int nranks, int image_layout, float *d_out,
+                            void *stream);
+
 /* ---- output (VRT/stb_image_write.h:178,723-757) ------------------------- */
 /* Byte-identical to stbi_write_hdr: returns 1 on success, 0 on failure. */
 int vrt_write_hdr(const char *filename, int w, int h, int comp,

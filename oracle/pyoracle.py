@@ -61,6 +61,13 @@ def oracle():
             "ora_random_point_in_unit_sphere": (None, [C.POINTER(C.c_uint64), f32p]),
             "ora_render_secondary": (C.c_int64, [P, f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int,
                                                  C.c_int, f32p, i32p, i32p, u32p]),
+            "ora_lightmap": (C.c_int64, [P, f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int]),
+            "ora_lightmap_filter": (None, [P]),
+            "ora_lightmap_nodes": (None, [P, C.POINTER(C.c_uint64), f32p, f32p]),
+            "ora_min_voxel": (C.c_float, [P, C.c_int]),
+            "ora_shade_trace": (None, [P, f32p, C.c_int, C.c_float, f32p]),
+            "ora_render_trace": (None, [P, f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_float, C.c_int,
+                                        f32p, i32p, f32p]),
         }
         for k, (res, args) in sig.items():
             f = getattr(L, k)
@@ -270,6 +277,7 @@ class Scene:
     def __init__(self, sd, max_depth):
         L = oracle()
         self.sd = sd
+        self.max_depth = int(max_depth)
         uv = sd.uv if sd.uv is not None else np.zeros((sd.ntri, 6), np.float32)
         mat = sd.mat if sd.mat is not None else np.zeros(sd.ntri, np.int32)
         self._uv, self._mat = np.ascontiguousarray(uv), np.ascontiguousarray(mat)
@@ -356,3 +364,40 @@ class Scene:
         sec = oracle().ora_render_rows(self.h, _p(cam, f32p), film_w, film_h, nx, ny, row_stride,
                                        row_phase, nthreads, _p(rgb, f32p))
         return sec, rgb
+
+    # ---- full trace() ----
+    def lightmap(self, cam, film_w, film_h, nx, ny, nthreads=8, filter=True):
+        """Light pass in canonical order (+ cone_trace_init_filter); returns hits."""
+        hits = oracle().ora_lightmap(self.h, _p(cam, f32p), film_w, film_h, nx, ny, nthreads)
+        if filter:
+            oracle().ora_lightmap_filter(self.h)
+        return hits
+
+    def lightmap_nodes(self):
+        """(key depth<<32|vox, coverage, illum (n,6,3)) sorted by key."""
+        n = int(self.info()[0][0])
+        key = np.zeros(n, np.uint64)
+        cov = np.zeros(n, np.float32)
+        ill = np.zeros((n, 6, 3), np.float32)
+        oracle().ora_lightmap_nodes(self.h, key.ctypes.data_as(C.POINTER(C.c_uint64)), _p(cov, f32p),
+                                    _p(ill, f32p))
+        o = np.argsort(key, kind="stable")
+        return key[o], cov[o], ill[o]
+
+    def min_voxel(self, levels=None):
+        return float(oracle().ora_min_voxel(self.h, self.max_depth if levels is None else int(levels)))
+
+    def shade_trace(self, rays, res):
+        rays = np.ascontiguousarray(np.asarray(rays, np.float32).reshape(-1, 8))
+        out = np.zeros((rays.shape[0], 3), np.float32)
+        oracle().ora_shade_trace(self.h, _p(rays, f32p), rays.shape[0], res, _p(out, f32p))
+        return out
+
+    def render_trace(self, cam, film_w, film_h, nx, ny, res, nthreads=8, samples=True):
+        rgb = np.zeros((ny, nx, 3), np.float32)
+        ns = nx * ny * 4
+        hit = np.zeros(ns, np.int32) if samples else None
+        srgb = np.zeros((ns, 3), np.float32) if samples else None
+        oracle().ora_render_trace(self.h, _p(cam, f32p), film_w, film_h, nx, ny, res, nthreads, _p(rgb, f32p),
+                                  _p(hit, i32p), _p(srgb, f32p))
+        return (rgb, {"hit": hit, "rgb": srgb}) if samples else rgb

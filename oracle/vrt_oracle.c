@@ -369,6 +369,8 @@ struct ora_scene {
         omat *mats;
         otex *texs;
         uint8_t *texbytes;
+        float *lm_cov;    /* VoxelOctree::coverage per node (full trace) */
+        float *lm_illum;  /* VoxelOctree::illum[6] per node, 18 floats */
 };
 
 static int new_node(ora_scene *s)
@@ -537,6 +539,8 @@ void ora_scene_destroy(ora_scene *s)
         free(s->mats);
         free(s->texs);
         free(s->texbytes);
+        free(s->lm_cov);
+        free(s->lm_illum);
         free(s);
 }
 
@@ -1157,4 +1161,358 @@ int64_t ora_render_secondary(const ora_scene *s, const float cam[19],
                 free(th);
         }
         return (int64_t)atomic_load(&j.rays);
+}
+
+/* ------------------------------------------------------------------ */
+/* Full trace(): light map, filter, cone tracing     */
+/* ------------------------------------------------------------------ */
+/* VoxelOctree::illum_d (VRT/voxel_octree.cc:19-20) */
+static const float kIllumD[6][3] = { { 1, 0, 0 },  { 0, 1, 0 },  { 0, 0, 1 },
+                                     { -1, 0, 0 }, { 0, -1, 0 }, { 0, 0, -1 } };
+/* HemiCones (VRT/voxel_octree.cc:256-263): xyz direction, w weight */
+static const float kHemi[6][4] = {
+        { 0.000000f, 0.000000f, 1.0f, 0.25f },  { 0.000000f, 0.866025f, 0.5f, 0.15f },
+        { 0.823639f, 0.267617f, 0.5f, 0.15f },  { 0.509037f, -0.700629f, 0.5f, 0.15f },
+        { -0.509037f, -0.700629f, 0.5f, 0.15f }, { -0.823639f, 0.267617f, 0.5f, 0.15f },
+};
+
+typedef struct {
+        int leaf;   /* -1: no hit */
+        v3 illum;   /* get_diffuse(isect, ray, (1,1,1)) */
+        v3 normal;  /* isect.normal */
+} lsample;
+
+typedef struct {
+        const ora_scene *s;
+        const float *cam;
+        float fw, fh;
+        int nx, ny;
+        lsample *out;
+        atomic_int next;
+} ljob;
+
+/* One render_mt task of the light pass (VRT/main.cc:80-97): task
+ * t = tx*8 + ty in post order (VRT/camera.h:50-56), pixels row-major,
+ * gen_rays4 samples in order.  Sample k of the canonical single-threaded
+ * order is stored at out[k]. */
+static void *light_worker(void *arg)
+{
+        ljob *j = arg;
+        const int ptx = j->nx / 8, pty = j->ny / 8;
+        for (;;) {
+                const int t = atomic_fetch_add(&j->next, 1);
+                if (t >= 64)
+                        break;
+                const int tx = t / 8, ty = t % 8;
+                size_t k = (size_t)t * (size_t)ptx * (size_t)pty * 4;
+                for (int py = pty * ty; py < pty * ty + pty; ++py)
+                        for (int px = ptx * tx; px < ptx * tx + ptx; ++px) {
+                                float rays[32];
+                                ora_gen_rays4(j->cam, j->fw, j->fh, j->nx, j->ny, px, py, rays);
+                                for (int q = 0; q < 4; ++q, ++k) {
+                                        omarch m;
+                                        const float *r = rays + 8 * q;
+                                        lsample *o = &j->out[k];
+                                        if (!ray_march(j->s, r, &m)) {
+                                                o->leaf = -1;
+                                                continue;
+                                        }
+                                        o->leaf = m.leaf;
+                                        o->illum = shade_sample(j->s, r, 1, &m);
+                                        o->normal = m.is.normal;
+                                }
+                        }
+        }
+        return NULL;
+}
+
+int64_t ora_lightmap(ora_scene *s, const float cam[19], float film_w,
+                     float film_h, int nx, int ny, int nthreads)
+{
+        free(s->lm_cov);
+        free(s->lm_illum);
+        s->lm_cov = calloc((size_t)s->nnodes, sizeof(float));
+        s->lm_illum = calloc((size_t)s->nnodes * 18, sizeof(float));
+        const size_t ns = (size_t)(nx / 8) * (size_t)(ny / 8) * 64 * 4;
+        ljob j;
+        memset(&j, 0, sizeof j);
+        j.s = s;
+        j.cam = cam;
+        j.fw = film_w;
+        j.fh = film_h;
+        j.nx = nx;
+        j.ny = ny;
+        j.out = malloc(sizeof(lsample) * (ns ? ns : 1));
+        atomic_init(&j.next, 0);
+        if (nthreads <= 1) {
+                light_worker(&j);
+        } else {
+                pthread_t *th = malloc(sizeof(pthread_t) * (size_t)nthreads);
+                for (int i = 0; i < nthreads; ++i)
+                        pthread_create(&th[i], NULL, light_worker, &j);
+                for (int i = 0; i < nthreads; ++i)
+                        pthread_join(th[i], NULL);
+                free(th);
+        }
+        /* leaf_ptr->illum[i] += clamp(dot(illum_d[i], n), 0, 1) * illum in
+         * the canonical order (the reference's += is racy across tasks) */
+        int64_t hits = 0;
+        for (size_t k = 0; k < ns; ++k) {
+                const lsample *o = &j.out[k];
+                if (o->leaf < 0)
+                        continue;
+                ++hits;
+                float *L = s->lm_illum + 18 * (size_t)o->leaf;
+                for (int i = 0; i < 6; ++i) {
+                        float coeff = dot(vget(kIllumD[i]), o->normal);
+                        coeff = clampf_(coeff, 0.f, 1.f);
+                        v3 acc = add(vget(L + 3 * i), muls(o->illum, coeff));
+                        L[3 * i + 0] = acc.x;
+                        L[3 * i + 1] = acc.y;
+                        L[3 * i + 2] = acc.z;
+                }
+        }
+        free(j.out);
+        return hits;
+}
+
+/* cone_trace_init_filter (VRT/voxel_octree.cc:190-214) */
+static void filter_node(ora_scene *s, int ni)
+{
+        onode *nd = &s->nodes[ni];
+        float *L = s->lm_illum + 18 * (size_t)ni;
+        if (nd->child < 0) {
+                if (nd->ntris == 0) {
+                        s->lm_cov[ni] = 0;
+                        memset(L, 0, sizeof(float) * 18);
+                        return;
+                }
+                s->lm_cov[ni] = 1.f;
+                return;
+        }
+        s->lm_cov[ni] = 0.f;
+        memset(L, 0, sizeof(float) * 18);
+        const int first = nd->child;
+        for (int i = 0; i < 8; ++i) {
+                filter_node(s, first + i);
+                s->lm_cov[ni] += s->lm_cov[first + i];
+                const float *C = s->lm_illum + 18 * (size_t)(first + i);
+                for (int f = 0; f < 18; ++f)
+                        L[f] += C[f];
+        }
+        for (int f = 0; f < 18; ++f)
+                L[f] /= 8; /* Vec3 /= 8 */
+        s->lm_cov[ni] /= 8.f;
+}
+
+void ora_lightmap_filter(ora_scene *s)
+{
+        if (!s->lm_cov) {
+                s->lm_cov = calloc((size_t)s->nnodes, sizeof(float));
+                s->lm_illum = calloc((size_t)s->nnodes * 18, sizeof(float));
+        }
+        filter_node(s, 0);
+}
+
+void ora_lightmap_nodes(const ora_scene *s, uint64_t *key, float *cov,
+                        float *illum)
+{
+        for (int i = 0; i < s->nnodes; ++i) {
+                const onode *n = &s->nodes[i];
+                key[i] = ((uint64_t)n->depth << 32) | vox_key(n);
+                if (cov) cov[i] = s->lm_cov ? s->lm_cov[i] : 0.f;
+                if (illum)
+                        for (int f = 0; f < 18; ++f)
+                                illum[18 * (size_t)i + f] = s->lm_illum ? s->lm_illum[18 * (size_t)i + f] : 0.f;
+        }
+}
+
+/* VoxelOctree::compute_illum (VRT/voxel_octree.h:72-82) */
+static v3 compute_illum(const ora_scene *s, int ni, v3 d)
+{
+        v3 r = mk(0, 0, 0);
+        const float *L = s->lm_illum + 18 * (size_t)ni;
+        for (int i = 0; i < 6; ++i) {
+                float coeff = dot(vget(kIllumD[i]), d);
+                coeff = clampf_(coeff, 0.f, 1.f);
+                r = add(r, muls(vget(L + 3 * i), coeff));
+        }
+        return r;
+}
+
+/* cone_trace(root, cone, min_voxel_size) (VRT/voxel_octree.cc:276-311) */
+static v3 cone_march(const ora_scene *s, v3 o, v3 d, float min_voxel)
+{
+        const float aperture = 0.577350269f, step = .1f, decay = 1.f;
+        const float mindist = 1.414f * min_voxel;
+        const float *rb = s->nodes[0].box;
+        const float maxdist = length(sub(vget(rb + 3), vget(rb)));
+        float dist = mindist;
+        float opacity = 0.f;
+        v3 diffuse = mk(0, 0, 0);
+        while (dist < maxdist && opacity < 1.f) {
+                const v3 p = add(o, muls(d, dist));
+                const float diam = stdmax(mindist, aperture * 2.f * dist);
+                if (maxdist < diam)
+                        break;
+                int split_level = (int)log2f(maxdist / diam);
+                int ni = 0;
+                while (s->nodes[ni].child >= 0 && split_level) {
+                        const float *b = s->nodes[ni].box;
+                        const v3 c = muls(add(vget(b), vget(b + 3)), .5f);
+                        int i = 0;
+                        i += (p.x > c.x ? 4 : 0);
+                        i += (p.y > c.y ? 2 : 0);
+                        i += (p.z > c.z ? 1 : 0);
+                        ni = s->nodes[ni].child + i;
+                        split_level--;
+                }
+                if (split_level == 0) {
+                        const v3 illum = compute_illum(s, ni, neg(d));
+                        const float transparency = clampf_(1.f - opacity, 0.f, 1.f);
+                        const float cov = s->lm_cov[ni];
+                        const float a = cov * step;
+                        const float w = (1.f / (1 + decay * dist)) * transparency * cov;
+                        diffuse = add(diffuse, muls(illum, w));
+                        opacity += transparency * a;
+                }
+                dist += step * diam;
+        }
+        return diffuse;
+}
+
+/* cone_trace(root, isect, min_voxel_size) (VRT/voxel_octree.cc:313-330)
+ * with orthonormal_basis (VRT/voxel_octree.cc:265-274) */
+static v3 cone_trace_isect(const ora_scene *s, v3 hit, v3 n, float min_voxel)
+{
+        const float sg = (0.0f > n.z) ? -1.0f : 1.0f;
+        const float a0 = -1.0f / (sg + n.z);
+        const float a1 = n.x * n.y * a0;
+        const v3 t = mk(1.0f + sg * n.x * n.x * a0, sg * a1, -sg * n.x);
+        const v3 b = mk(a1, sg + n.y * n.y * a0, -n.y);
+        v3 diffuse = mk(0, 0, 0);
+        for (int i = 0; i < 6; ++i) {
+                /* dot(Mat3{t,b,n}, d) = ((0 + t*d.x) + b*d.y) + n*d.z */
+                v3 r = mk(0, 0, 0);
+                r = add(r, muls(t, kHemi[i][0]));
+                r = add(r, muls(b, kHemi[i][1]));
+                r = add(r, muls(n, kHemi[i][2]));
+                const v3 cd = normalize(r);
+                diffuse = add(diffuse, muls(cone_march(s, hit, cd, min_voxel), kHemi[i][3]));
+        }
+        return diffuse;
+}
+
+float ora_min_voxel(const ora_scene *s, int levels)
+{
+        const float *rb = s->nodes[0].box;
+        const float p2 = powf(2.f, (float)levels);
+        float res = (rb[3] - rb[0]) / p2;
+        if ((rb[4] - rb[1]) / p2 < res) res = (rb[4] - rb[1]) / p2;
+        if ((rb[5] - rb[2]) / p2 < res) res = (rb[5] - rb[2]) / p2;
+        return res;
+}
+
+/* trace(root, ray, 5, true) (VRT/main.cc:10-30) */
+static v3 trace_sample(const ora_scene *s, const float r[8], float res,
+                       omarch *m, int *h)
+{
+        *h = ray_march(s, r, m);
+        if (!*h)
+                return shade_sample(s, r, 0, m);
+        const v3 indirect = cone_trace_isect(s, m->is.hit, m->is.normal, res);
+        const v3 direct = compute_illum(s, m->leaf, neg(vget(r + 3)));
+        const v3 albedo = get_albedo(s, m->tri, m->is.hit);
+        const v3 l = add(indirect, direct);
+        return mk(albedo.x * l.x, albedo.y * l.y, albedo.z * l.z);
+}
+
+void ora_shade_trace(const ora_scene *s, const float *rays, int n, float res,
+                     float *rgb)
+{
+        for (int i = 0; i < n; ++i) {
+                omarch m;
+                int h;
+                v3 c = trace_sample(s, rays + 8 * i, res, &m, &h);
+                rgb[3 * i + 0] = c.x;
+                rgb[3 * i + 1] = c.y;
+                rgb[3 * i + 2] = c.z;
+        }
+}
+
+typedef struct {
+        const ora_scene *s;
+        const float *cam;
+        float fw, fh, res;
+        int nx, ny;
+        float *rgb, *s_rgb;
+        int32_t *s_hit;
+        atomic_int next;
+} tjob;
+
+static void *trace_worker(void *arg)
+{
+        tjob *j = arg;
+        const int ptx = j->nx / 8, pty = j->ny / 8;
+        for (;;) {
+                const int t = atomic_fetch_add(&j->next, 1);
+                if (t >= 64)
+                        break;
+                const int tx = t / 8, ty = t % 8;
+                for (int py = pty * ty; py < pty * ty + pty; ++py)
+                        for (int px = ptx * tx; px < ptx * tx + ptx; ++px) {
+                                float rays[32];
+                                ora_gen_rays4(j->cam, j->fw, j->fh, j->nx, j->ny, px, py, rays);
+                                for (int q = 0; q < 4; ++q) {
+                                        omarch m;
+                                        int h;
+                                        const v3 c = trace_sample(j->s, rays + 8 * q, j->res, &m, &h);
+                                        const size_t si = ((size_t)py * j->nx + px) * 4 + q;
+                                        if (j->s_hit) j->s_hit[si] = h;
+                                        if (j->s_rgb) {
+                                                j->s_rgb[3 * si + 0] = c.x;
+                                                j->s_rgb[3 * si + 1] = c.y;
+                                                j->s_rgb[3 * si + 2] = c.z;
+                                        }
+                                        float *o = j->rgb + ((size_t)py * j->nx + px) * 3;
+                                        o[0] += c.x * .25f;
+                                        o[1] += c.y * .25f;
+                                        o[2] += c.z * .25f;
+                                }
+                        }
+        }
+        return NULL;
+}
+
+void ora_render_trace(const ora_scene *s, const float cam[19], float film_w,
+                      float film_h, int nx, int ny, float res, int nthreads,
+                      float *rgb, int32_t *s_hit, float *s_rgb)
+{
+        tjob j;
+        memset(&j, 0, sizeof j);
+        j.s = s;
+        j.cam = cam;
+        j.fw = film_w;
+        j.fh = film_h;
+        j.res = res;
+        j.nx = nx;
+        j.ny = ny;
+        j.rgb = rgb;
+        j.s_rgb = s_rgb;
+        j.s_hit = s_hit;
+        memset(rgb, 0, sizeof(float) * 3 * (size_t)nx * ny);
+        const size_t ns = (size_t)nx * ny * 4;
+        if (s_hit) memset(s_hit, 0, sizeof(int32_t) * ns);
+        if (s_rgb) memset(s_rgb, 0, sizeof(float) * 3 * ns);
+        atomic_init(&j.next, 0);
+        if (nthreads <= 1) {
+                trace_worker(&j);
+        } else {
+                pthread_t *th = malloc(sizeof(pthread_t) * (size_t)nthreads);
+                for (int i = 0; i < nthreads; ++i)
+                        pthread_create(&th[i], NULL, trace_worker, &j);
+                for (int i = 0; i < nthreads; ++i)
+                        pthread_join(th[i], NULL);
+                free(th);
+        }
 }

@@ -132,6 +132,32 @@ int64_t ora_render_secondary(const ora_scene *s, const float cam[19],
                              int spp, int nthreads, float *vis,
                              int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox);
 
+/* ---- full trace() ------------------------------------
+ * Light pass (VRT/main.cc:79-97): render_mt over the light film with
+ * gen_rays4; every hit adds clamp(dot(illum_d[i], n), 0, 1) * get_diffuse
+ * to leaf_ptr->illum[i].  The reference's += is racy across its thread
+ * pool; here the sums run in the canonical single-threaded order (task
+ * t = tx*8+ty, pixels row-major, samples 0..3).  Returns the hit count. */
+int64_t ora_lightmap(ora_scene *s, const float cam[19], float film_w,
+                     float film_h, int nx, int ny, int nthreads);
+/* cone_trace_init_filter (VRT/voxel_octree.cc:190-214). */
+void ora_lightmap_filter(ora_scene *s);
+/* Per node (oracle order): key = depth<<32 | ix | iy<<10 | iz<<20 at its
+ * depth, coverage, illum[6][3]. */
+void ora_lightmap_nodes(const ora_scene *s, uint64_t *key, float *cov,
+                        float *illum);
+/* min component of root.size() / powf(2, levels) (VRT/main.cc:69-70). */
+float ora_min_voxel(const ora_scene *s, int levels);
+/* trace(root, ray, 5, true) per ray (VRT/main.cc:10-30): sky on a miss,
+ * else get_albedo * (cone_trace(root, isect, res) + leaf compute_illum(-d)). */
+void ora_shade_trace(const ora_scene *s, const float *rays, int n, float res,
+                     float *rgb);
+/* The cone-tracing render (VRT/main.cc:114-123): rgb nx*ny*3 (index
+ * y*nx+x), optional per-sample s_hit / s_rgb ((py*nx+px)*4+s). */
+void ora_render_trace(const ora_scene *s, const float cam[19], float film_w,
+                      float film_h, int nx, int ny, float res, int nthreads,
+                      float *rgb, int32_t *s_hit, float *s_rgb);
+
 /* stbiw__linear_to_rgbe (VRT/stb_image_write.h:601-616) for one pixel. */
 void ora_linear_to_rgbe(const float linear[3], uint8_t rgbe[4]);
 

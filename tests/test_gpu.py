@@ -300,3 +300,52 @@ def test_device_rgbe_pack_matches_reference_writer(tmp_path):
         assert vrt.write_hdr_device(p, d.data_ptr(), w, h, comp)
         want = z[f"bytes{i}"].tobytes() if i < 6 else vrt.hdr_bytes(img)
         assert p.read_bytes() == want, i
+
+
+# ---- full trace() ----
+LIGHT = (vrt.to_radian(60), (1.0, 10.0, 1.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0))  # VRT/main.cc:80-83
+
+
+@pytest.mark.parametrize("depth,light_n", [(5, 96), (6, 128), (8, 256)])
+def test_lightmap_and_trace_match_oracle(proxy_small, depth, light_n):
+    """Light pass + filter: every node's coverage and illum[6] bit-exact vs
+    the oracle's canonical-order sums; then the cone-tracing render."""
+    tree = vrt.VoxelOctree(proxy_small, depth)
+    osc = po.Scene(proxy_small, depth)
+    hits = tree.lightmap(vrt.Camera(*LIGHT), vrt.Film(1, 1, light_n, light_n))
+    ohits = osc.lightmap(po.camera(*LIGHT), 1.0, 1.0, light_n, light_n, nthreads=8)
+    assert hits == ohits > 0
+    k, cov, ill = tree.lightmap_nodes()
+    ok, ocov, oill = osc.lightmap_nodes()
+    assert np.array_equal(k, ok)
+    assert np.array_equal(bits(cov), bits(ocov))
+    assert np.array_equal(bits(ill), bits(oill))
+    res = tree.min_voxel(6)
+    assert res == osc.min_voxel(6)
+    mn, mx = tree.root_box
+    cams = [(vrt.to_radian(90), (1.0, 1.3, -0.2), (0.0, 0.4, 0.0), (0.0, 1.0, 0.0))]
+    cams += [vrt.sweep_pose(mn, mx, i, 16) for i in (3, 10)]
+    for fov, eye, spot, up in cams:
+        rgb, so = tree.render_trace(vrt.Camera(fov, eye, spot, up), vrt.Film(1, 1, 40, 32), res, samples=True)
+        orgb, oso = osc.render_trace(po.camera(fov, eye, spot, up), 1.0, 1.0, 40, 32, res, nthreads=8)
+        assert np.array_equal(so["hit"], oso["hit"])
+        assert np.array_equal(bits(so["rgb"]), bits(oso["rgb"]))
+        assert np.array_equal(bits(rgb), bits(orgb))
+
+
+def test_trace_device_tiles_reassemble(proxy_small):
+    import torch
+    tree = vrt.VoxelOctree(proxy_small, 6)
+    tree.lightmap(vrt.Camera(*LIGHT), vrt.Film(1, 1, 64, 64))
+    cam = vrt.Camera(vrt.to_radian(90), (1.0, 1.3, -0.2), (0.0, 0.4, 0.0), (0.0, 1.0, 0.0))
+    film = vrt.Film(1, 1, 48, 40)
+    direct = tree.render_trace(cam, film)
+    n = 3
+    tpr = vrt.tiles_per_rank(film, n)
+    g = torch.zeros(n * tpr * 192, device="cuda")
+    for r in range(n):
+        tree.render_trace_device(cam, film, r, n, 0, g[r * tpr * 192:].data_ptr())
+    img = torch.zeros(48 * 40 * 3, device="cuda")
+    vrt.unpack_tiles_device(film, n, g.data_ptr(), img.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(img.cpu().numpy().reshape(40, 48, 3)), bits(direct))

@@ -256,3 +256,19 @@ def test_tiles_per_rank():
     assert vrt.tiles_per_rank(f, 1) == 240 * 135
     assert vrt.tiles_per_rank(f, 8) == (240 * 135 + 7) // 8
     assert vrt.tiles_per_rank(vrt.Film(1, 1, 7, 7), 1) == 0
+
+
+def test_trace_api_host_only_scene():
+    """min_voxel matches the oracle's Res; device-only trace calls on a
+    host-only scene fail with VRT_E_NODEVICE (no CPU fallback)."""
+    sd = vrt.SceneData.proxy(0.05, 1)
+    tree = vrt.VoxelOctree(sd, 6, device=-1)
+    osc = po.Scene(sd, 6)
+    for lv in (0, 4, 6, 9):
+        assert tree.min_voxel(lv) == osc.min_voxel(lv if lv else 6)
+    cam = vrt.Camera(vrt.to_radian(60), (1, 10, 1), (0, 0, 0), (0, 1, 0))
+    with pytest.raises(vrt.VrtError) as e:
+        tree.lightmap(cam, vrt.Film(1, 1, 64, 64))
+    assert e.value.status == vrt._ffi.VRT_E_NODEVICE
+    with pytest.raises(vrt.VrtError):
+        tree.render_trace(cam, vrt.Film(1, 1, 16, 16))

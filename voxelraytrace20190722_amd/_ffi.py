@@ -121,6 +121,12 @@ SIGNATURES = {
     "vrt_proxy_scene": (C.c_int, [C.c_double, C.c_uint32, i32p, f32p, f32p, f32p, i32p,
                                   i32p, i32p, f32p, i32p, i32p, i64p, u8p, i64p]),
     "vrt_sweep_pose": (C.c_int, [f32p, f32p, C.c_int, C.c_int, f32p, f32p, f32p, f32p]),
+    "vrt_lightmap_build": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), i64p]),
+    "vrt_lightmap_nodes": (C.c_int, [_P, C.POINTER(C.c_uint64), f32p, f32p]),
+    "vrt_scene_min_voxel": (C.c_int, [_P, C.c_int, f32p]),
+    "vrt_render_trace": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), C.c_float, f32p, i32p, f32p]),
+    "vrt_render_trace_device": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), C.c_float, C.c_int, C.c_int,
+                                          C.c_int, _P, _P]),
     "vrt_obj_load": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_P)]),
     "vrt_obj_free": (None, [_P]),
     "vrt_obj_info": (C.c_int, [_P, C.POINTER(ObjInfo)]),

@@ -392,6 +392,48 @@ class VoxelOctree:
         check(lib().vrt_last_kernel_ms(self.h, C.byref(ms)), "vrt_last_kernel_ms")
         return ms.value
 
+    # ---- full trace() ----
+    def min_voxel(self, levels=0):
+        """The reference's Res: min(root.size() / 2^levels) (VRT/main.cc:69-70)."""
+        r = C.c_float()
+        check(lib().vrt_scene_min_voxel(self.h, int(levels), C.byref(r)), "vrt_scene_min_voxel")
+        return r.value
+
+    def lightmap(self, light_cam, light_film):
+        """Light pass + cone_trace_init_filter on the device; returns hit samples."""
+        h = C.c_int64()
+        check(lib().vrt_lightmap_build(self.h, C.byref(light_cam.c), C.byref(light_film.c), C.byref(h)),
+              "vrt_lightmap_build")
+        return h.value
+
+    def lightmap_nodes(self):
+        """(key depth<<32|vox, coverage, illum (n,6,3)) sorted by key."""
+        n = self.info.nodes
+        key = np.zeros(n, np.uint64)
+        cov = np.zeros(n, np.float32)
+        ill = np.zeros((n, 6, 3), np.float32)
+        check(lib().vrt_lightmap_nodes(self.h, key.ctypes.data_as(C.POINTER(C.c_uint64)), ptr(cov, _ffi.f32p),
+                                       ptr(ill, _ffi.f32p)), "vrt_lightmap_nodes")
+        o = np.argsort(key, kind="stable")
+        return key[o], cov[o], ill[o]
+
+    def render_trace(self, cam, film, min_voxel=0.0, samples=False):
+        """trace() render (cone tracing) -> (ny, nx, 3) [+ per-sample hit / rgb]."""
+        rgb = np.zeros((film.ny, film.nx, 3), np.float32)
+        ns = film.nx * film.ny * 4
+        hit = np.zeros(ns, np.int32) if samples else None
+        srgb = np.zeros((ns, 3), np.float32) if samples else None
+        check(lib().vrt_render_trace(self.h, C.byref(cam.c), C.byref(film.c), float(min_voxel), ptr(rgb, _ffi.f32p),
+                                     ptr(hit, _ffi.i32p), ptr(srgb, _ffi.f32p)), "vrt_render_trace")
+        return (rgb, {"hit": hit, "rgb": srgb}) if samples else rgb
+
+    def render_trace_device(self, cam, film, rank, nranks, image_layout, d_out_ptr, min_voxel=0.0,
+                            stream_ptr=None):
+        check(lib().vrt_render_trace_device(self.h, C.byref(cam.c), C.byref(film.c), float(min_voxel), int(rank),
+                                            int(nranks), int(image_layout), C.c_void_p(d_out_ptr),
+                                            None if stream_ptr is None else C.c_void_p(stream_ptr)),
+              "vrt_render_trace_device")
+
 
 def ray_march_init(scene, max_depth, device=0):
     """gi::ray_march_init(root, voxels, max_depth) (VRT/voxel_octree.cc:67-75)."""

@@ -312,6 +312,12 @@ struct vrt_scene {
         std::vector<TexRec> texs;
         int64_t tex_bytes = 0;
         vrt_scene_info_t info{};
+        std::vector<int64_t> level_begin;  // BFS level l (1-based) = [lb[l-1], lb[l])
+        // full trace: per-node light map + light-pass scratch (device)
+        LMRec *d_lm = nullptr;
+        bool lm_ready = false;
+        void *d_light = nullptr;
+        size_t light_bytes = 0;
         // device
         void *d_mem = nullptr;
         DevScene dev{};
@@ -425,7 +431,9 @@ static int build_tree(vrt_scene *s, const vrt_scene_desc *d)
         // level l's nodes occupy a contiguous index range [lv_begin, lv_end)
         int64_t lv_begin = 0, lv_end = 1;
         size_t ref_pos = 0;
+        s->level_begin.clear();
         for (int l = 1; l <= D; ++l) {
+                s->level_begin.push_back(lv_begin);
                 const std::vector<uint32_t> &I = internal[l];  // empty at l == D
                 // nodes of this level are in code order (children blocks of
                 // the previous level's code-ordered internal nodes)
@@ -475,6 +483,7 @@ static int build_tree(vrt_scene *s, const vrt_scene_desc *d)
                 if (l < D && lv_begin == lv_end)
                         break;
         }
+        s->level_begin.push_back(nnodes);
         // content masks, bottom-up (children always follow their parent):
         // an internal node's b = the children that hold triangles somewhere
         // below.  The kernels never push a child outside this mask: a
@@ -722,12 +731,16 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
 {
         if (!s)
                 return;
-        if (s->d_mem || s->stream || s->ev0 || s->ev1) {
+        if (s->d_mem || s->d_lm || s->d_light || s->stream || s->ev0 || s->ev1) {
                 (void)hipSetDevice(s->device);
                 if (s->stream)
                         (void)hipStreamSynchronize(s->stream);
                 if (s->d_mem)
                         (void)hipFree(s->d_mem);
+                if (s->d_lm)
+                        (void)hipFree(s->d_lm);
+                if (s->d_light)
+                        (void)hipFree(s->d_light);
                 if (s->ev0)
                         (void)hipEventDestroy(s->ev0);
                 if (s->ev1)
@@ -1067,6 +1080,262 @@ extern "C" int vrt_render_secondary(vrt_scene *s, const vrt_camera *cam,
                         hits += prim[8 * i] != 0.f;
                 *rays = (int64_t)narea + hits * spp;
         }
+        return VRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// full trace(): light map, filter, cone-tracing render
+// ---------------------------------------------------------------------------
+// (int)log2f(x) thresholds of the host libm: split_up[e] = smallest float in
+// [2^e, 2^(e+1)) whose log2f rounds up to e+1 (+inf if none).  The cone
+// march (VRT/voxel_octree.cc:286) truncates log2f; the device evaluates the
+// same integer from x's exponent and this table.
+static const float *split_table()
+{
+        static float tab[64];
+        static std::once_flag once;
+        std::call_once(once, [] {
+                for (int e = 0; e < 64; ++e) {
+                        const float lo = std::ldexp(1.0f, e), top = std::ldexp(1.0f, e + 1);
+                        float t = INFINITY;
+                        for (float x = std::nextafter(top, 0.0f); x >= lo; x = std::nextafter(x, 0.0f)) {
+                                volatile float xv = x;
+                                if ((int)log2f(xv) != e + 1)
+                                        break;
+                                t = x;
+                        }
+                        tab[e] = t;
+                }
+        });
+        return tab;
+}
+
+extern "C" int vrt_scene_min_voxel(const vrt_scene *s, int levels, float *res)
+{
+        if (!s || !res)
+                return fail(VRT_E_INVALID, "null argument");
+        const float p2 = std::pow(2.f, (float)(levels > 0 ? levels : s->max_depth));
+        for (int k = 0; k < 3; ++k) {
+                const float v = (s->info.root_max[k] - s->info.root_min[k]) / p2;
+                if (k == 0 || v < *res)
+                        *res = v;
+        }
+        return VRT_OK;
+}
+
+static hipError_t ensure_light_scratch(vrt_scene *s, size_t bytes)
+{
+        if (s->light_bytes >= bytes)
+                return hipSuccess;
+        if (s->d_light) {
+                hipError_t e = hipStreamSynchronize(s->stream);
+                if (e != hipSuccess)
+                        return e;
+                (void)hipFree(s->d_light);
+                s->d_light = nullptr;
+                s->light_bytes = 0;
+        }
+        hipError_t e = hipMalloc(&s->d_light, bytes);
+        if (e == hipSuccess)
+                s->light_bytes = bytes;
+        return e;
+}
+
+extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
+                                  const vrt_film *light_film, int64_t *hits)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !light_cam)
+                return fail(VRT_E_INVALID, "null argument");
+        if (int rc = film_ok(light_film))
+                return rc;
+        std::lock_guard<std::mutex> lk(s->mu);
+        HIPCHK(hipSetDevice(s->device));
+        const int64_t nnodes = (int64_t)s->nodes.size();
+        const int ptx = light_film->nx / 8, pty = light_film->ny / 8;
+        const int64_t ns = (int64_t)64 * ptx * pty * 4;
+        if (ns > 0x7FFFFFFF)
+                return fail(VRT_E_INVALID, "light film too large (%lld samples)", (long long)ns);
+        if (!s->d_lm)
+                HIPCHK(hipMalloc(reinterpret_cast<void **>(&s->d_lm), (size_t)nnodes * sizeof(LMRec)));
+        HIPCHK(hipMemsetAsync(s->d_lm, 0, (size_t)nnodes * sizeof(LMRec), s->stream));
+        // scratch: keys/vals in+out, per-sample (illum, normal), sort temp
+        size_t sort_bytes = 0;
+        const uint32_t miss_key = (uint32_t)nnodes;
+        int bits = 1;
+        while (bits < 32 && (miss_key >> bits) != 0)
+                ++bits;
+        HIPCHK(sort_pairs_u32(nullptr, &sort_bytes, nullptr, nullptr, nullptr, nullptr, ns, bits, s->stream));
+        const size_t b4 = align_up((size_t)ns * 4), b24 = align_up((size_t)ns * 24);
+        const size_t need = 4 * b4 + b24 + align_up(sort_bytes) + 256;
+        HIPCHK(ensure_light_scratch(s, need));
+        char *base = static_cast<char *>(s->d_light);
+        uint32_t *k_in = reinterpret_cast<uint32_t *>(base);
+        uint32_t *k_out = reinterpret_cast<uint32_t *>(base + b4);
+        uint32_t *v_in = reinterpret_cast<uint32_t *>(base + 2 * b4);
+        uint32_t *v_out = reinterpret_cast<uint32_t *>(base + 3 * b4);
+        float *samp = reinterpret_cast<float *>(base + 4 * b4);
+        void *temp = base + 4 * b4 + b24;
+        unsigned long long *d_hits = reinterpret_cast<unsigned long long *>(base + 4 * b4 + b24 + align_up(sort_bytes));
+        HIPCHK(hipMemsetAsync(d_hits, 0, sizeof(unsigned long long), s->stream));
+        LightParams lp;
+        std::memset(&lp, 0, sizeof lp);
+        fill_render_params(s, light_cam, light_film, 0, 1, &lp.r);
+        lp.ptx = ptx;
+        lp.pty = pty;
+        lp.miss_key = miss_key;
+        lp.keys = k_in;
+        lp.samp = samp;
+        lp.hits = d_hits;
+        HIPCHK(hipEventRecord(s->ev0, s->stream));
+        HIPCHK(launch_light(lp, s->stream));
+        HIPCHK(launch_iota(v_in, ns, s->stream));
+        HIPCHK(sort_pairs_u32(temp, &sort_bytes, k_in, k_out, v_in, v_out, ns, bits, s->stream));
+        HIPCHK(launch_lm_accum(ns, k_out, v_out, samp, miss_key, s->d_lm, s->stream));
+        // cone_trace_init_filter: leaves, then internal levels bottom-up
+        HIPCHK(launch_lm_leaves(s->dev.nodes, nnodes, s->d_lm, s->stream));
+        const int nlev = (int)s->level_begin.size() - 1;
+        for (int l = nlev; l >= 1; --l)
+                HIPCHK(launch_lm_level(s->dev.nodes, s->level_begin[l - 1], s->level_begin[l], s->d_lm, s->stream));
+        HIPCHK(hipEventRecord(s->ev1, s->stream));
+        s->timed = true;
+        unsigned long long h = 0;
+        HIPCHK(hipMemcpyAsync(&h, d_hits, sizeof h, hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        if (hits)
+                *hits = (int64_t)h;
+        s->lm_ready = true;
+        return VRT_OK;
+}
+
+extern "C" int vrt_lightmap_nodes(vrt_scene *s, uint64_t *key, float *coverage, float *illum)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !key)
+                return fail(VRT_E_INVALID, "null argument");
+        if (!s->lm_ready)
+                return fail(VRT_E_INVALID, "no light map: call vrt_lightmap_build first");
+        std::lock_guard<std::mutex> lk(s->mu);
+        HIPCHK(hipSetDevice(s->device));
+        const size_t n = s->nodes.size();
+        std::vector<LMRec> lm(n);
+        HIPCHK(hipMemcpy(lm.data(), s->d_lm, n * sizeof(LMRec), hipMemcpyDeviceToHost));
+        for (size_t l = 0; l + 1 < s->level_begin.size(); ++l)
+                for (int64_t i = s->level_begin[l]; i < s->level_begin[l + 1]; ++i) {
+                        key[i] = ((uint64_t)(l + 1) << 32) | s->node_vox[(size_t)i];
+                        if (coverage)
+                                coverage[i] = lm[(size_t)i].cov;
+                        if (illum)
+                                std::memcpy(illum + 18 * (size_t)i, lm[(size_t)i].illum, 18 * sizeof(float));
+                }
+        return VRT_OK;
+}
+
+static int trace_ok(vrt_scene *s, float min_voxel)
+{
+        if (!(min_voxel > 0.f))
+                vrt_scene_min_voxel(s, 0, &min_voxel);
+        const float mindist = 1.414f * min_voxel;
+        if (!(mindist > 0.f) || !std::isfinite(mindist))
+                return fail(VRT_E_INVALID, "degenerate cone step: min voxel %g (flat scene?)", (double)min_voxel);
+        for (int k = 0; k < 3; ++k)
+                if (!std::isfinite(s->info.root_max[k] - s->info.root_min[k]))
+                        return fail(VRT_E_INVALID, "scene bounds not finite");
+        return VRT_OK;
+}
+
+static void fill_trace_params(vrt_scene *s, const vrt_camera *cam, const vrt_film *film, float min_voxel,
+                              int rank, int nranks, TraceParams *tp)
+{
+        std::memset(tp, 0, sizeof *tp);
+        fill_render_params(s, cam, film, rank, nranks, &tp->r);
+        if (!(min_voxel > 0.f))
+                vrt_scene_min_voxel(s, 0, &min_voxel);
+        tp->lm = s->d_lm;
+        // float mindist = 1.414f * min_voxel_size; maxdist = length(root.aabb.size())
+        tp->mindist = 1.414f * min_voxel;
+        const f3 sz = mk3(s->info.root_max[0] - s->info.root_min[0], s->info.root_max[1] - s->info.root_min[1],
+                          s->info.root_max[2] - s->info.root_min[2]);
+        tp->maxdist = length(sz);
+        std::memcpy(tp->split_up, split_table(), sizeof tp->split_up);
+}
+
+extern "C" int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam, const vrt_film *film,
+                                       float min_voxel, int rank, int nranks, int image_layout,
+                                       float *d_out, void *stream)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !cam || !d_out)
+                return fail(VRT_E_INVALID, "null argument");
+        if (int rc = film_ok(film))
+                return rc;
+        if (!s->lm_ready)
+                return fail(VRT_E_INVALID, "no light map: call vrt_lightmap_build first");
+        if (nranks < 1 || rank < 0 || rank >= nranks)
+                return fail(VRT_E_INVALID, "rank %d of %d", rank, nranks);
+        if (image_layout && nranks != 1)
+                return fail(VRT_E_INVALID, "image_layout requires nranks == 1");
+        if (int rc = trace_ok(s, min_voxel))
+                return rc;
+        HIPCHK(hipSetDevice(s->device));
+        TraceParams tp;
+        fill_trace_params(s, cam, film, min_voxel, rank, nranks, &tp);
+        tp.r.image_layout = image_layout;
+        tp.r.out = d_out;
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        HIPCHK(hipEventRecord(s->ev0, st));
+        HIPCHK(launch_trace(tp, st));
+        HIPCHK(hipEventRecord(s->ev1, st));
+        s->timed = true;
+        return VRT_OK;
+}
+
+extern "C" int vrt_render_trace(vrt_scene *s, const vrt_camera *cam, const vrt_film *film, float min_voxel,
+                                float *rgb, int32_t *s_hit, float *s_rgb)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !cam || !rgb)
+                return fail(VRT_E_INVALID, "null argument");
+        if (int rc = film_ok(film))
+                return rc;
+        if (!s->lm_ready)
+                return fail(VRT_E_INVALID, "no light map: call vrt_lightmap_build first");
+        if (int rc = trace_ok(s, min_voxel))
+                return rc;
+        std::lock_guard<std::mutex> lk(s->mu);
+        HIPCHK(hipSetDevice(s->device));
+        const size_t npix = (size_t)film->nx * film->ny, ns = npix * 4;
+        DevBuf img, dh, dr;
+        HIPCHK(hipMalloc(&img.p, npix * 12));
+        HIPCHK(hipMemsetAsync(img.p, 0, npix * 12, s->stream));
+        TraceParams tp;
+        fill_trace_params(s, cam, film, min_voxel, 0, 1, &tp);
+        tp.r.image_layout = 1;
+        tp.r.out = static_cast<float *>(img.p);
+        if (s_hit) {
+                HIPCHK(hipMalloc(&dh.p, ns * 4));
+                HIPCHK(hipMemsetAsync(dh.p, 0, ns * 4, s->stream));
+                tp.r.so.hit = static_cast<int32_t *>(dh.p);
+        }
+        if (s_rgb) {
+                HIPCHK(hipMalloc(&dr.p, ns * 12));
+                HIPCHK(hipMemsetAsync(dr.p, 0, ns * 12, s->stream));
+                tp.r.so.rgb = static_cast<float *>(dr.p);
+        }
+        HIPCHK(hipEventRecord(s->ev0, s->stream));
+        HIPCHK(launch_trace(tp, s->stream));
+        HIPCHK(hipEventRecord(s->ev1, s->stream));
+        s->timed = true;
+        HIPCHK(hipStreamSynchronize(s->stream));
+        HIPCHK(hipMemcpy(rgb, img.p, npix * 12, hipMemcpyDeviceToHost));
+        if (s_hit)
+                HIPCHK(hipMemcpy(s_hit, dh.p, ns * 4, hipMemcpyDeviceToHost));
+        if (s_rgb)
+                HIPCHK(hipMemcpy(s_rgb, dr.p, ns * 12, hipMemcpyDeviceToHost));
         return VRT_OK;
 }
 

@@ -100,6 +100,40 @@ struct RenderParams {
         SampleOut so;
 };
 
+// ---- full trace() -------------------------------------
+// Per-node cone-tracing state (80 B): VoxelOctree::coverage and illum[6]
+// (VRT/voxel_octree.h:64-70), indexed like NodeRec.
+struct alignas(16) LMRec {
+        float cov;
+        float illum[18];
+        float pad;
+};
+static_assert(sizeof(LMRec) == 80, "LMRec must be 80 B");
+
+// Light pass (VRT/main.cc:79-97) over r's film: every sample of the
+// canonical single-threaded order k (render_mt task t = tx*8+ty of
+// ptx x pty pixels, row-major, samples 0..3) writes keys[k] = hit leaf node
+// (~0u on a miss) and samp[6k..6k+5] = get_diffuse rgb, isect normal.
+struct LightParams {
+        RenderParams r;
+        int32_t ptx, pty;
+        uint32_t miss_key;   // key of a miss (= node count: sorts last)
+        uint32_t *keys;
+        float *samp;
+        unsigned long long *hits;  // += hit samples
+};
+
+// Cone-tracing render (trace(), VRT/main.cc:10-30 + cone_trace,
+// VRT/voxel_octree.cc:276-330).  split_up[e]: smallest float x in
+// [2^e, 2^(e+1)) with (int)log2f(x) == e+1 under the host libm (the same
+// log2f the oracle and the reference's float path call), +inf if none.
+struct TraceParams {
+        RenderParams r;
+        const LMRec *lm;
+        float mindist, maxdist;
+        float split_up[64];
+};
+
 // Kernel launchers (vrt_kernels.hip)
 hipError_t launch_render(const RenderParams &p, bool instrumented,
                          hipStream_t st);
@@ -112,6 +146,17 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,
                             int nranks, float res, float *prim, float *vis,
                             int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox,
                             hipStream_t st);
+hipError_t launch_light(const LightParams &p, hipStream_t st);
+hipError_t launch_lm_accum(int64_t n, const uint32_t *keys_sorted, const uint32_t *vals_sorted,
+                           const float *samp, uint32_t miss_key, LMRec *lm, hipStream_t st);
+hipError_t launch_lm_leaves(const NodeRec *nodes, int64_t nnodes, LMRec *lm, hipStream_t st);
+hipError_t launch_lm_level(const NodeRec *nodes, int64_t begin, int64_t end, LMRec *lm, hipStream_t st);
+hipError_t launch_trace(const TraceParams &p, hipStream_t st);
+// stable radix sort of (key, value) pairs on the low `bits` key bits
+// (vrt_sort.hip); temp == nullptr queries *temp_bytes
+hipError_t sort_pairs_u32(void *temp, size_t *temp_bytes, const uint32_t *keys_in, uint32_t *keys_out,
+                          const uint32_t *vals_in, uint32_t *vals_out, int64_t n, int bits, hipStream_t st);
+hipError_t launch_iota(uint32_t *v, int64_t n, hipStream_t st);
 hipError_t launch_rgbe(const float *img, int64_t npx, int comp, uint8_t *out, hipStream_t st);
 hipError_t launch_selftest(const double *mt_in, double *mt_out,
                            const float *sat_in, int32_t *sat_out, int64_t n,

@@ -578,10 +578,9 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
                 ray_march<kCount, false>(sc, r, sb, so, sa, pr, m);
 }
 
-// Triangle::get_diffuse(isect, ray, (1,1,1)) (VRT/voxel_octree.cc:462-484)
-// with Triangle::isect's normal (VRT/voxel_octree.cc:451-453).
-__device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
-                                        const MarchResult &m, f3 &normal)
+// Triangle::get_albedo (VRT/voxel_octree.cc:472-484) with Triangle::isect's
+// normal (VRT/voxel_octree.cc:451-453).
+__device__ __forceinline__ f3 hit_albedo(const DevScene &sc, const MarchResult &m, f3 &normal)
 {
         const TriAttr *ta = sc.tri_attr + m.tri;
         const float4 *q = reinterpret_cast<const float4 *>(ta);
@@ -619,6 +618,14 @@ __device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
                 const float c2 = tx.c > 2 ? (float)p[2] : 0.f;
                 albedo = mk3(c0 / 255.f, c1 / 255.f, c2 / 255.f);
         }
+        return albedo;
+}
+
+// Triangle::get_diffuse(isect, ray, (1,1,1)) (VRT/voxel_octree.cc:462-470)
+__device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
+                                        const MarchResult &m, f3 &normal)
+{
+        const f3 albedo = hit_albedo(sc, m, normal);
         float tmp = dot(normal, -r.d);
         tmp = clampf(tmp, 0.f, 1.f);
         const f3 c = albedo * tmp;
@@ -1098,6 +1105,376 @@ hipError_t launch_selftest(const double *mt_in, double *mt_out,
                 return hipSuccess;
         hipLaunchKernelGGL(k_selftest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                            mt_in, mt_out, sat_in, sat_out, n);
+        return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------
+// Full trace(): light pass, light-map accumulation in the
+// canonical order, cone_trace_init_filter, cone-tracing render.
+// ---------------------------------------------------------------------------
+// VoxelOctree::illum_d (VRT/voxel_octree.cc:19-20)
+__device__ __forceinline__ f3 illum_dir(int i)
+{
+        const float v = i < 3 ? 1.f : -1.f;
+        const int ax = i % 3;
+        return mk3(ax == 0 ? v : 0.f, ax == 1 ? v : 0.f, ax == 2 ? v : 0.f);
+}
+
+// XCD-aware 8x8-pixel tile of this block and this lane's pixel / sample
+// (the k_render mapping).  Returns false for padding blocks.
+__device__ __forceinline__ bool tile_lane(const RenderParams &p, int &k, int &px, int &py,
+                                          int &s, int &lx, int &ly)
+{
+        const int nb = gridDim.x, b = blockIdx.x;
+        const int per = (nb + 7) >> 3;
+        k = ((nb & 7) != 0) ? b : (b & 7) * per + (b >> 3);
+        if (k >= p.tiles_this_rank)
+                return false;
+        const int t = p.rank + k * p.nranks;
+        const int tx = t % p.ntx, ty = t / p.ntx;
+        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        s = lane & 3;
+        const int pix = lane >> 2;
+        lx = (wave & 1) * 4 + (pix & 3);
+        ly = (wave >> 1) * 4 + (pix >> 2);
+        px = tx * 8 + lx;
+        py = ty * 8 + ly;
+        return true;
+}
+
+__global__ __launch_bounds__(kBlock) void k_light(LightParams p)
+{
+        __shared__ uint32_t stk_base[kStack * kBlock];
+        __shared__ uint32_t stk_ord[kStack * kBlock];
+        const int tid = threadIdx.x;
+        int k, px, py, s, lx, ly;
+        if (!tile_lane(p.r, k, px, py, s, lx, ly))
+                return;
+        const CamParams &c = p.r.cam;
+        const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
+                                 sample_x(s), sample_y(s));
+        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
+                                 dn, c.tmin, c.tmax);
+        MarchResult m;
+        ray_march_dispatch<false>(p.r.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        // canonical order: render_mt task t = tx*8 + ty (VRT/camera.h:50-56)
+        const int tx = px / p.ptx, ty = py / p.pty;
+        const int64_t task = (int64_t)tx * 8 + ty;
+        const int64_t key = ((task * p.pty + (py - ty * p.pty)) * p.ptx + (px - tx * p.ptx)) * 4 + s;
+        const unsigned long long wave_hits = __popcll(__ballot(m.hit));
+        if ((tid & 63) == 0 && wave_hits)
+                atomicAdd(p.hits, wave_hits);
+        if (!m.hit) {
+                p.keys[key] = p.miss_key;
+                return;
+        }
+        f3 nrm;
+        const f3 il = shade_hit(p.r.sc, r, m, nrm);
+        p.keys[key] = m.node;
+        float *o = p.samp + 6 * key;
+        o[0] = il.x; o[1] = il.y; o[2] = il.z;
+        o[3] = nrm.x; o[4] = nrm.y; o[5] = nrm.z;
+}
+
+// One thread per run of equal leaf keys (stable-sorted, so the run is in
+// canonical sample order): leaf_ptr->illum[i] += clamp(dot(illum_d[i], n),
+// 0, 1) * illum (VRT/main.cc:90-95), starting from zero.
+__global__ __launch_bounds__(256) void k_lm_accum(int64_t n, const uint32_t *__restrict__ keys,
+                                                  const uint32_t *__restrict__ vals,
+                                                  const float *__restrict__ samp, uint32_t miss_key,
+                                                  LMRec *__restrict__ lm)
+{
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= n)
+                return;
+        const uint32_t leaf = keys[i];
+        if (leaf >= miss_key || (i > 0 && keys[i - 1] == leaf))
+                return;
+        float acc[18];
+#pragma unroll
+        for (int f = 0; f < 18; ++f)
+                acc[f] = 0.f;
+        for (int64_t j = i; j < n && keys[j] == leaf; ++j) {
+                const float *q = samp + 6 * (int64_t)vals[j];
+                const f3 il = mk3(q[0], q[1], q[2]);
+                const f3 nn = mk3(q[3], q[4], q[5]);
+#pragma unroll
+                for (int d = 0; d < 6; ++d) {
+                        float coeff = dot(illum_dir(d), nn);
+                        coeff = clampf(coeff, 0.f, 1.f);
+                        acc[3 * d + 0] = acc[3 * d + 0] + coeff * il.x;
+                        acc[3 * d + 1] = acc[3 * d + 1] + coeff * il.y;
+                        acc[3 * d + 2] = acc[3 * d + 2] + coeff * il.z;
+                }
+        }
+#pragma unroll
+        for (int f = 0; f < 18; ++f)
+                lm[leaf].illum[f] = acc[f];
+}
+
+// cone_trace_init_filter, leaf case (VRT/voxel_octree.cc:192-200)
+__global__ __launch_bounds__(256) void k_lm_leaves(const NodeRec *__restrict__ nodes, int64_t n,
+                                                   LMRec *__restrict__ lm)
+{
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= n)
+                return;
+        const uint32_t a = nodes[i].a;
+        if (!(a & kLeafBit))
+                return;
+        if ((a & ~kLeafBit) == 0) {
+                lm[i].cov = 0.f;
+#pragma unroll
+                for (int f = 0; f < 18; ++f)
+                        lm[i].illum[f] = 0.f;
+        } else {
+                lm[i].cov = 1.f;
+        }
+}
+
+// cone_trace_init_filter, internal case for one BFS level (children in
+// order 0..7 summed from zero, then / 8; VRT/voxel_octree.cc:201-213)
+__global__ __launch_bounds__(256) void k_lm_level(const NodeRec *__restrict__ nodes, int64_t begin,
+                                                  int64_t end, LMRec *__restrict__ lm)
+{
+        const int64_t i = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= end)
+                return;
+        const uint32_t a = nodes[i].a;
+        if (a & kLeafBit)
+                return;
+        float cov = 0.f;
+        float acc[18];
+#pragma unroll
+        for (int f = 0; f < 18; ++f)
+                acc[f] = 0.f;
+        for (int c = 0; c < 8; ++c) {
+                const LMRec &ch = lm[a + c];
+                cov += ch.cov;
+#pragma unroll
+                for (int f = 0; f < 18; ++f)
+                        acc[f] += ch.illum[f];
+        }
+#pragma unroll
+        for (int f = 0; f < 18; ++f)
+                lm[i].illum[f] = acc[f] / 8.0f;
+        lm[i].cov = cov / 8.f;
+}
+
+// VoxelOctree::compute_illum (VRT/voxel_octree.h:72-82)
+__device__ __forceinline__ f3 compute_illum(const LMRec *__restrict__ lm, uint32_t ni, f3 d)
+{
+        const float4 *q = reinterpret_cast<const float4 *>(lm + ni);
+        const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
+        const float L[18] = { q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y,
+                              q2.z, q2.w, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, q4.z };
+        f3 r = mk3(0.f, 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+                float coeff = dot(illum_dir(i), d);
+                coeff = clampf(coeff, 0.f, 1.f);
+                r = mk3(r.x + coeff * L[3 * i + 0], r.y + coeff * L[3 * i + 1], r.z + coeff * L[3 * i + 2]);
+        }
+        return r;
+}
+
+// (int)log2f(x) for x >= 1 through the host-libm threshold table
+__device__ __forceinline__ int split_level_of(float x, const float *up)
+{
+        const int e = (int)(__float_as_uint(x) >> 23) - 127;
+        if (e >= 63)
+                return e;  // unreachable for finite scenes (maxdist/mindist < 2^63)
+        return x >= up[e] ? e + 1 : e;
+}
+
+// cone_trace(root, cone, min_voxel_size) (VRT/voxel_octree.cc:276-311)
+__device__ __forceinline__ f3 cone_march(const TraceParams &p, f3 o, f3 d)
+{
+        const float aperture = 0.577350269f, step = .1f, decay = 1.f;
+        const NodeRec *__restrict__ nodes = p.r.sc.nodes;
+        const f3 nd = -d;
+        float dist = p.mindist;
+        float opacity = 0.f;
+        f3 diffuse = mk3(0.f, 0.f, 0.f);
+        // (the host rejects mindist <= 0, which would never terminate; the
+        // step cap is a guard only: dist grows >= 11% per step)
+        for (int guard = 0; dist < p.maxdist && opacity < 1.f && guard < (1 << 16); ++guard) {
+                const f3 pt = o + d * dist;
+                const float diam = std_max(p.mindist, aperture * 2.f * dist);
+                if (p.maxdist < diam)
+                        break;
+                int split = split_level_of(p.maxdist / diam, p.split_up);
+                uint32_t ni = 0;
+                float bmin[3], bmax[3];
+                uint32_t a, b;
+                load_node(nodes, 0, bmin, bmax, a, b);
+                while (!(a & kLeafBit) && split) {
+                        const float cx = (bmin[0] + bmax[0]) * .5f;
+                        const float cy = (bmin[1] + bmax[1]) * .5f;
+                        const float cz = (bmin[2] + bmax[2]) * .5f;
+                        int i = 0;
+                        i += (pt.x > cx ? 4 : 0);
+                        i += (pt.y > cy ? 2 : 0);
+                        i += (pt.z > cz ? 1 : 0);
+                        ni = a + (uint32_t)i;
+                        load_node(nodes, ni, bmin, bmax, a, b);
+                        split--;
+                }
+                if (split == 0) {
+                        const f3 il = compute_illum(p.lm, ni, nd);
+                        const float transparency = clampf(1.f - opacity, 0.f, 1.f);
+                        const float cov = p.lm[ni].cov;
+                        const float aa = cov * step;
+                        const float w = (1.f / (1.f + decay * dist)) * transparency * cov;
+                        diffuse = mk3(diffuse.x + w * il.x, diffuse.y + w * il.y, diffuse.z + w * il.z);
+                        opacity += transparency * aa;
+                }
+                dist += step * diam;
+        }
+        return diffuse;
+}
+
+// cone_trace(root, isect, min_voxel_size) with orthonormal_basis
+// (VRT/voxel_octree.cc:256-274, 313-330)
+__device__ __forceinline__ f3 cone_trace_isect(const TraceParams &p, f3 hit, f3 n)
+{
+        const float hx[6] = { 0.000000f, 0.000000f, 0.823639f, 0.509037f, -0.509037f, -0.823639f };
+        const float hy[6] = { 0.000000f, 0.866025f, 0.267617f, -0.700629f, -0.700629f, 0.267617f };
+        const float hz[6] = { 1.0f, 0.5f, 0.5f, 0.5f, 0.5f, 0.5f };
+        const float hw[6] = { 0.25f, 0.15f, 0.15f, 0.15f, 0.15f, 0.15f };
+        const float sg = (0.0f > n.z) ? -1.0f : 1.0f;
+        const float a0 = -1.0f / (sg + n.z);
+        const float a1 = n.x * n.y * a0;
+        const f3 t = mk3(1.0f + sg * n.x * n.x * a0, sg * a1, -sg * n.x);
+        const f3 bb = mk3(a1, sg + n.y * n.y * a0, -n.y);
+        f3 diffuse = mk3(0.f, 0.f, 0.f);
+        for (int i = 0; i < 6; ++i) {
+                f3 r = mk3(0.f, 0.f, 0.f);
+                r = r + t * hx[i];
+                r = r + bb * hy[i];
+                r = r + n * hz[i];
+                const f3 cd = normalize(r);
+                const f3 cm = cone_march(p, hit, cd);
+                diffuse = diffuse + cm * hw[i];
+        }
+        return diffuse;
+}
+
+// trace(root, ray, 5, true) per sample + Film::add(c * .25f)
+// (VRT/main.cc:10-30, 118-123)
+__global__ __launch_bounds__(kBlock) void k_trace(TraceParams p)
+{
+        __shared__ uint32_t stk_base[kStack * kBlock];
+        __shared__ uint32_t stk_ord[kStack * kBlock];
+        const int tid = threadIdx.x, lane = tid & 63;
+        int k, px, py, s, lx, ly;
+        if (!tile_lane(p.r, k, px, py, s, lx, ly))
+                return;
+        const CamParams &c = p.r.cam;
+        const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
+                                 sample_x(s), sample_y(s));
+        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
+                                 dn, c.tmin, c.tmax);
+        MarchResult m;
+        ray_march_dispatch<false>(p.r.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        f3 col;
+        if (m.hit) {
+                f3 nrm;
+                const f3 albedo = hit_albedo(p.r.sc, m, nrm);
+                const f3 indirect = cone_trace_isect(p, m.hp, nrm);
+                const f3 direct = compute_illum(p.lm, m.node, -r.d);
+                const f3 l = indirect + direct;
+                col = mk3(albedo.x * l.x, albedo.y * l.y, albedo.z * l.z);
+        } else {
+                col = sky(r.d.y);
+        }
+        const size_t si = ((size_t)py * c.nx + px) * 4 + s;
+        if (p.r.so.hit) p.r.so.hit[si] = m.hit ? 1 : 0;
+        if (p.r.so.rgb) {
+                p.r.so.rgb[3 * si + 0] = col.x;
+                p.r.so.rgb[3 * si + 1] = col.y;
+                p.r.so.rgb[3 * si + 2] = col.z;
+        }
+        const f3 cq = col * .25f;
+        const int l0 = lane & ~3;
+        float acc[3] = { 0.0f, 0.0f, 0.0f };
+        const float cv[3] = { cq.x, cq.y, cq.z };
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                        acc[q] += __shfl(cv[q], l0 + j, 64);
+        }
+        if (s == 0) {
+                float *o;
+                if (p.r.image_layout)
+                        o = p.r.out + ((size_t)py * c.nx + px) * 3;
+                else
+                        o = p.r.out + ((size_t)k * 64 + ly * 8 + lx) * 3;
+                o[0] = acc[0];
+                o[1] = acc[1];
+                o[2] = acc[2];
+        }
+}
+
+__global__ void k_iota(uint32_t *v, int64_t n)
+{
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i < n)
+                v[i] = (uint32_t)i;
+}
+
+hipError_t launch_light(const LightParams &p, hipStream_t st)
+{
+        if (p.r.tiles_this_rank <= 0)
+                return hipSuccess;
+        const int grid = (p.r.tiles_this_rank + 7) & ~7;
+        hipLaunchKernelGGL(k_light, dim3(grid), dim3(kBlock), 0, st, p);
+        return hipGetLastError();
+}
+
+hipError_t launch_lm_accum(int64_t n, const uint32_t *keys_sorted, const uint32_t *vals_sorted,
+                           const float *samp, uint32_t miss_key, LMRec *lm, hipStream_t st)
+{
+        if (n <= 0)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_lm_accum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, keys_sorted,
+                           vals_sorted, samp, miss_key, lm);
+        return hipGetLastError();
+}
+
+hipError_t launch_lm_leaves(const NodeRec *nodes, int64_t nnodes, LMRec *lm, hipStream_t st)
+{
+        if (nnodes <= 0)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_lm_leaves, dim3((unsigned)((nnodes + 255) / 256)), dim3(256), 0, st, nodes, nnodes, lm);
+        return hipGetLastError();
+}
+
+hipError_t launch_lm_level(const NodeRec *nodes, int64_t begin, int64_t end, LMRec *lm, hipStream_t st)
+{
+        if (end <= begin)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_lm_level, dim3((unsigned)((end - begin + 255) / 256)), dim3(256), 0, st, nodes, begin,
+                           end, lm);
+        return hipGetLastError();
+}
+
+hipError_t launch_trace(const TraceParams &p, hipStream_t st)
+{
+        if (p.r.tiles_this_rank <= 0)
+                return hipSuccess;
+        const int grid = (p.r.tiles_this_rank + 7) & ~7;
+        hipLaunchKernelGGL(k_trace, dim3(grid), dim3(kBlock), 0, st, p);
+        return hipGetLastError();
+}
+
+hipError_t launch_iota(uint32_t *v, int64_t n, hipStream_t st)
+{
+        if (n <= 0)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_iota, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, n);
         return hipGetLastError();
 }
 
