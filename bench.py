@@ -42,23 +42,31 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=32)
     p.add_argument("--warmup", type=int, default=4)
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
-    p.add_argument("--depth", type=int, default=8, help="max_depth; '256^3' = log2(256) = 8")
+    p.add_argument("--width", type=int, default=None, help="default 1920 (1024 for --mode trace)")
+    p.add_argument("--height", type=int, default=None, help="default 1080 (1024 for --mode trace)")
+    p.add_argument("--depth", type=int, default=None,
+                   help="max_depth; default 8 = '256^3' (6 for --mode trace, as VRT/main.cc:67)")
+    p.add_argument("--light-n", type=int, default=2048, help="light film side (--mode trace, VRT/main.cc:79)")
     p.add_argument("--detail", type=float, default=1.0, help="proxy tessellation (1.0 ~ 262k tris)")
     p.add_argument("--poses", type=int, default=16)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-counters", action="store_true")
-    p.add_argument("--mode", default="primary", choices=["primary", "secondary"],
-                   help="primary: BASELINE configs 1-4 (4 spp primary render); secondary: config 5")
+    p.add_argument("--mode", default="primary", choices=["primary", "secondary", "trace"],
+                   help="primary: BASELINE configs 1-4 (4 spp primary render); secondary: config 5; "
+                        "trace: the reference's full main() frame (light map + filter + cone tracing)")
     p.add_argument("--spp", type=int, default=64, help="secondary rays per hit pixel (--mode secondary)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (RCCL over xGMI, the real path) or gloo (host-staged rehearsal)")
     p.add_argument("--save-image", default="", help="rank 0 writes the last frame as .hdr")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return p.parse_args()
+    a = p.parse_args()
+    trace = a.mode == "trace"
+    a.width = a.width or (1024 if trace else 1920)
+    a.height = a.height or (1024 if trace else 1080)
+    a.depth = a.depth or (6 if trace else 8)
+    return a
 
 
 def main():
@@ -91,6 +99,15 @@ def main():
     for i in range(a.poses):
         fov, eye, spot, up = vrt.sweep_pose(mn, mx, i, a.poses)
         cams.append(vrt.Camera(fov, eye, spot, up))
+    trace = a.mode == "trace"
+    if trace:
+        # VRT/main.cc:79-83 (light camera + film) and :108-112 (view camera)
+        light_cam = vrt.Camera(vrt.to_radian(60), (1, 10, 1), (0, 0, 0), (0, 1, 0))
+        light_film = vrt.Film(1, 1, a.light_n, a.light_n)
+        cams = [vrt.Camera(vrt.to_radian(90), (1.0, 1.3, -0.2), (0.0, 0.4, 0.0), (0.0, 1.0, 0.0))]
+        a.poses = 1
+        res = tree.min_voxel(a.depth)
+        light_ms = []
     film = vrt.Film(1.0, 1.0, a.width, a.height)
     W8, H8 = 8 * (a.width // 8), 8 * (a.height // 8)
     rays_per_frame = W8 * H8 * 4
@@ -159,20 +176,34 @@ def main():
             if rank == 0:
                 img.copy_(host)
 
+    def render(cam, rk, nr, layout, ptr_):
+        if trace:
+            tree.render_trace_device(cam, film, rk, nr, layout, ptr_, res, sp)
+        else:
+            tree.render_tiles_device(cam, film, rk, nr, layout, ptr_, sp)
+
     def step(k, timed):
         if secondary:
             return step_secondary(k, timed)
         cam = cams[k % a.poses]
+        if trace:
+            # light pass + filter (blocking, on the scene's own stream; every
+            # rank builds the whole light map -- the final render is sharded)
+            torch.cuda.current_stream(dev).synchronize()
+            t0_ = time.perf_counter()
+            tree.lightmap(light_cam, light_film)
+            if timed:
+                light_ms.append((time.perf_counter() - t0_) * 1e3)
         if timed:
             ev[k][0].record(stream)
         if world == 1:
-            tree.render_tiles_device(cam, film, 0, 1, 1, img.data_ptr(), sp)
+            render(cam, 0, 1, 1, img.data_ptr())
             if timed:
                 ev[k][1].record(stream)
             return
         b = k & 1
         finish(b)  # frame k-2 used this buffer pair
-        tree.render_tiles_device(cam, film, rank, world, 0, tiles[b].data_ptr(), sp)
+        render(cam, rank, world, 0, tiles[b].data_ptr())
         if timed:
             ev[k][1].record(stream)
         finish(1 - b)  # frame k-1: its gather overlapped this render
@@ -215,7 +246,7 @@ def main():
     # ---- algorithmic bytes from the instrumented kernel's
     # reference-equivalent counters, per pose actually rendered
     roof = None
-    if not a.no_counters and not secondary:
+    if not a.no_counters and not secondary and not trace:
         poses_used = sorted({k % a.poses for k in range(a.steps)})
         b_rank = []
         cnt_tot = np.zeros(4)
@@ -253,7 +284,30 @@ def main():
     # ---- CPU baseline: the oracle (C restatement of the reference path,
     # render_mt-style 8x8 tiles over pthreads) on a bounded row sample
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu and not secondary:
+    if rank == 0 and world == 1 and not a.no_cpu and trace:
+        # one whole reference frame on the oracle: light pass (16 threads for
+        # the marches, canonical-order sums), filter, cone-tracing render
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as po
+        osc = po.Scene(sd, a.depth)
+        nth = max(1, min(a.cpu_threads, os.cpu_count() or 1))
+        t0_ = time.perf_counter()
+        osc.lightmap(po.camera(vrt.to_radian(60), (1, 10, 1), (0, 0, 0), (0, 1, 0)), 1.0, 1.0, a.light_n,
+                     a.light_n, nthreads=nth)
+        t1_ = time.perf_counter()
+        # bounded: the cone-traced view at half width and height (same camera,
+        # 1/4 of the samples), its time scaled x4 to the full film
+        hw, hh = a.width // 2, a.height // 2
+        osc.render_trace(po.camera(vrt.to_radian(90), (1.0, 1.3, -0.2), (0.0, 0.4, 0.0), (0.0, 1.0, 0.0)),
+                         1.0, 1.0, hw, hh, res, nthreads=nth, samples=False)
+        t2_ = time.perf_counter()
+        tr = (t2_ - t1_) * (a.width * a.height) / (hw * hh)
+        cpu = {"value": round(1.0 / ((t1_ - t0_) + tr), 5), "unit": "frames/s", "cores": nth, "kind": "port",
+               "sample": f"light map {a.light_n}^2 x4 + filter ({t1_ - t0_:.1f} s) + cone-traced {hw}x{hh} x4 "
+                         f"({t2_ - t1_:.1f} s, scaled x{(a.width * a.height) / (hw * hh):.0f} to "
+                         f"{a.width}x{a.height}) by oracle/vrt_oracle.c over {nth} threads"}
+        osc.close()
+    if rank == 0 and world == 1 and not a.no_cpu and not secondary and not trace:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle as po
         osc = po.Scene(sd, a.depth)
@@ -281,6 +335,28 @@ def main():
     if rank == 0:
         coll = "rccl" if a.dist_backend == "nccl" else "gloo"
         n_side = int(round(2 ** a.depth))
+        if trace:
+            value = a.steps / elapsed
+            out = {
+                "metric": f"frames/s of the reference main() frame: light map {a.light_n}^2 x4 + filter + "
+                          f"cone-traced {a.width}x{a.height} x4 (Sponza {int(round(2 ** a.depth))}^3 octree)",
+                "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": a.steps,
+                "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32+f64",
+                "data": "synthetic: deterministic sponza-proxy atrium (sponza.obj absent)",
+                "config": {"workload": f"full trace(): sponza-proxy ({sd.ntri} tris), max_depth {a.depth}",
+                           "mode": a.mode, "width": a.width, "height": a.height, "light_n": a.light_n,
+                           "max_depth": a.depth, "tris": sd.ntri,
+                           "parallelism": f"replicated light map, screen tiles x{world}"},
+                "light_ms_mean": round(float(np.mean(light_ms)), 3),
+                "trace_kernel_ms_mean": round(float(kms.mean()), 3),
+                "roofline": None,
+                "cpu_baseline": cpu,
+            }
+            print(json.dumps(out), flush=True)
+            if world > 1:
+                dist.destroy_process_group()
+            return
         if secondary:
             per_step = [frame_rays[k % a.poses] for k in range(a.steps)]
             total_rays = int(sum(per_step))
