@@ -1167,8 +1167,12 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         while (bits < 32 && (miss_key >> bits) != 0)
                 ++bits;
         HIPCHK(sort_pairs_u32(nullptr, &sort_bytes, nullptr, nullptr, nullptr, nullptr, ns, bits, s->stream));
-        const size_t b4 = align_up((size_t)ns * 4), b24 = align_up((size_t)ns * 24);
-        const size_t need = 4 * b4 + b24 + align_up(sort_bytes) + 256;
+        // samp holds the per-sample records and, right after them, their
+        // copy gathered into sorted order (launch_lm_accum)
+        const size_t b4 = align_up((size_t)ns * 4), b24 = align_up((size_t)ns * 48);
+        const int64_t max_seg = std::max<int64_t>(1, s->info.nonempty_leaves);
+        const size_t bseg = align_up((size_t)max_seg * 4);
+        const size_t need = 4 * b4 + b24 + align_up(sort_bytes) + 256 + bseg;
         HIPCHK(ensure_light_scratch(s, need));
         char *base = static_cast<char *>(s->d_light);
         uint32_t *k_in = reinterpret_cast<uint32_t *>(base);
@@ -1177,8 +1181,11 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         uint32_t *v_out = reinterpret_cast<uint32_t *>(base + 3 * b4);
         float *samp = reinterpret_cast<float *>(base + 4 * b4);
         void *temp = base + 4 * b4 + b24;
-        unsigned long long *d_hits = reinterpret_cast<unsigned long long *>(base + 4 * b4 + b24 + align_up(sort_bytes));
-        HIPCHK(hipMemsetAsync(d_hits, 0, sizeof(unsigned long long), s->stream));
+        char *tail = base + 4 * b4 + b24 + align_up(sort_bytes);
+        unsigned long long *d_hits = reinterpret_cast<unsigned long long *>(tail);
+        unsigned int *d_nseg = reinterpret_cast<unsigned int *>(tail + 64);
+        uint32_t *d_seg = reinterpret_cast<uint32_t *>(tail + 256);
+        HIPCHK(hipMemsetAsync(tail, 0, 256, s->stream));
         LightParams lp;
         std::memset(&lp, 0, sizeof lp);
         fill_render_params(s, light_cam, light_film, 0, 1, &lp.r);
@@ -1192,7 +1199,7 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         HIPCHK(launch_light(lp, s->stream));
         HIPCHK(launch_iota(v_in, ns, s->stream));
         HIPCHK(sort_pairs_u32(temp, &sort_bytes, k_in, k_out, v_in, v_out, ns, bits, s->stream));
-        HIPCHK(launch_lm_accum(ns, k_out, v_out, samp, miss_key, s->d_lm, s->stream));
+        HIPCHK(launch_lm_accum(ns, k_out, v_out, samp, miss_key, d_seg, d_nseg, max_seg, s->d_lm, s->stream));
         // cone_trace_init_filter: leaves, then internal levels bottom-up
         HIPCHK(launch_lm_leaves(s->dev.nodes, nnodes, s->d_lm, s->stream));
         const int nlev = (int)s->level_begin.size() - 1;

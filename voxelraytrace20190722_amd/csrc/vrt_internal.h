@@ -147,8 +147,11 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,
                             int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox,
                             hipStream_t st);
 hipError_t launch_light(const LightParams &p, hipStream_t st);
+// samp: n x 6 floats followed by room for their sorted copy (n x 6);
+// seg_start: max_seg entries (>= non-empty leaves), nseg zeroed
 hipError_t launch_lm_accum(int64_t n, const uint32_t *keys_sorted, const uint32_t *vals_sorted,
-                           const float *samp, uint32_t miss_key, LMRec *lm, hipStream_t st);
+                           const float *samp, uint32_t miss_key, uint32_t *seg_start, unsigned int *nseg,
+                           int64_t max_seg, LMRec *lm, hipStream_t st);
 hipError_t launch_lm_leaves(const NodeRec *nodes, int64_t nnodes, LMRec *lm, hipStream_t st);
 hipError_t launch_lm_level(const NodeRec *nodes, int64_t begin, int64_t end, LMRec *lm, hipStream_t st);
 hipError_t launch_trace(const TraceParams &p, hipStream_t st);

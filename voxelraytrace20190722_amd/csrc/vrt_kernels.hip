@@ -1177,13 +1177,25 @@ __global__ __launch_bounds__(kBlock) void k_light(LightParams p)
         o[3] = nrm.x; o[4] = nrm.y; o[5] = nrm.z;
 }
 
-// One thread per run of equal leaf keys (stable-sorted, so the run is in
-// canonical sample order): leaf_ptr->illum[i] += clamp(dot(illum_d[i], n),
-// 0, 1) * illum (VRT/main.cc:90-95), starting from zero.
-__global__ __launch_bounds__(256) void k_lm_accum(int64_t n, const uint32_t *__restrict__ keys,
-                                                  const uint32_t *__restrict__ vals,
-                                                  const float *__restrict__ samp, uint32_t miss_key,
-                                                  LMRec *__restrict__ lm)
+// Permute the per-sample records into the sorted (leaf, canonical) order so
+// the serial per-leaf sums below stream contiguous memory.
+__global__ __launch_bounds__(256) void k_lm_gather(int64_t n, const uint32_t *__restrict__ vals,
+                                                   const float *__restrict__ samp, float *__restrict__ out)
+{
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= n)
+                return;
+        const float2 *q = reinterpret_cast<const float2 *>(samp + 6 * (int64_t)vals[i]);
+        float2 *o = reinterpret_cast<float2 *>(out + 6 * i);
+        o[0] = q[0];
+        o[1] = q[1];
+        o[2] = q[2];
+}
+
+// Start index of every run of equal (hit) leaf keys; run order is irrelevant.
+__global__ __launch_bounds__(256) void k_lm_segments(int64_t n, const uint32_t *__restrict__ keys,
+                                                     uint32_t miss_key, uint32_t *__restrict__ seg_start,
+                                                     unsigned int *__restrict__ nseg)
 {
         const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
         if (i >= n)
@@ -1191,26 +1203,36 @@ __global__ __launch_bounds__(256) void k_lm_accum(int64_t n, const uint32_t *__r
         const uint32_t leaf = keys[i];
         if (leaf >= miss_key || (i > 0 && keys[i - 1] == leaf))
                 return;
-        float acc[18];
-#pragma unroll
-        for (int f = 0; f < 18; ++f)
-                acc[f] = 0.f;
-        for (int64_t j = i; j < n && keys[j] == leaf; ++j) {
-                const float *q = samp + 6 * (int64_t)vals[j];
-                const f3 il = mk3(q[0], q[1], q[2]);
-                const f3 nn = mk3(q[3], q[4], q[5]);
-#pragma unroll
-                for (int d = 0; d < 6; ++d) {
-                        float coeff = dot(illum_dir(d), nn);
-                        coeff = clampf(coeff, 0.f, 1.f);
-                        acc[3 * d + 0] = acc[3 * d + 0] + coeff * il.x;
-                        acc[3 * d + 1] = acc[3 * d + 1] + coeff * il.y;
-                        acc[3 * d + 2] = acc[3 * d + 2] + coeff * il.z;
-                }
+        seg_start[atomicAdd(nseg, 1u)] = (uint32_t)i;
+}
+
+// One 32-lane group per run (stable sort: the run is in canonical sample
+// order); lane 3d+c owns the running sum leaf->illum[d][c] and adds
+// clamp(dot(illum_d[d], n), 0, 1) * illum[c] sample by sample, from zero
+// (VRT/main.cc:90-95).  The 18 sums are independent, so they run side by
+// side; each stays a strictly sequential chain.
+__global__ __launch_bounds__(256) void k_lm_accum(int64_t n, const uint32_t *__restrict__ keys,
+                                                  const float *__restrict__ samp,
+                                                  const uint32_t *__restrict__ seg_start,
+                                                  const unsigned int *__restrict__ nseg,
+                                                  LMRec *__restrict__ lm)
+{
+        const uint32_t seg = blockIdx.x * 8 + (threadIdx.x >> 5);
+        const int l = threadIdx.x & 31;
+        if (seg >= *nseg || l >= 18)
+                return;
+        const int d = l / 3, c = l % 3;
+        const int64_t i0 = seg_start[seg];
+        const uint32_t leaf = keys[i0];
+        const f3 dir = illum_dir(d);
+        float acc = 0.f;
+        for (int64_t j = i0; j < n && keys[j] == leaf; ++j) {
+                const float *q = samp + 6 * j;  // gathered into sorted order
+                float coeff = dot(dir, mk3(q[3], q[4], q[5]));
+                coeff = clampf(coeff, 0.f, 1.f);
+                acc = acc + coeff * q[c];
         }
-#pragma unroll
-        for (int f = 0; f < 18; ++f)
-                lm[leaf].illum[f] = acc[f];
+        lm[leaf].illum[l] = acc;
 }
 
 // cone_trace_init_filter, leaf case (VRT/voxel_octree.cc:192-200)
@@ -1435,12 +1457,20 @@ hipError_t launch_light(const LightParams &p, hipStream_t st)
 }
 
 hipError_t launch_lm_accum(int64_t n, const uint32_t *keys_sorted, const uint32_t *vals_sorted,
-                           const float *samp, uint32_t miss_key, LMRec *lm, hipStream_t st)
+                           const float *samp, uint32_t miss_key, uint32_t *seg_start, unsigned int *nseg,
+                           int64_t max_seg, LMRec *lm, hipStream_t st)
 {
         if (n <= 0)
                 return hipSuccess;
-        hipLaunchKernelGGL(k_lm_accum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, keys_sorted,
-                           vals_sorted, samp, miss_key, lm);
+        // samp -> gathered copy directly after it (the caller sizes 2 x 24 B
+        // per sample)
+        float *sorted = const_cast<float *>(samp) + 6 * n;
+        const unsigned g = (unsigned)((n + 255) / 256);
+        hipLaunchKernelGGL(k_lm_gather, dim3(g), dim3(256), 0, st, n, vals_sorted, samp, sorted);
+        hipLaunchKernelGGL(k_lm_segments, dim3(g), dim3(256), 0, st, n, keys_sorted, miss_key, seg_start, nseg);
+        if (max_seg > 0)
+                hipLaunchKernelGGL(k_lm_accum, dim3((unsigned)((max_seg + 7) / 8)), dim3(256), 0, st, n, keys_sorted,
+                                   sorted, seg_start, nseg, lm);
         return hipGetLastError();
 }
 
