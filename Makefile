@@ -17,7 +17,7 @@ HIPFLAGS := -x hip --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 $(FP) -Iinclude -
 CXXFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Wall -fvisibility=hidden
 
 HOSTOBJS := $(BLD)/vrt_host.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o
-OBJS := $(BLD)/vrt_kernels.o $(BLD)/vrt_sort.o $(HOSTOBJS)
+OBJS := $(BLD)/vrt_kernels.o $(BLD)/vrt_sort.o $(BLD)/vrt_build.o $(HOSTOBJS)
 HDRS := include/vrt.h $(SRC)/vrt_math.h $(SRC)/vrt_internal.h $(SRC)/vrt_error.h
 
 all: $(PKG)/libvrt.so oracle
@@ -29,6 +29,9 @@ $(BLD)/vrt_kernels.o: $(SRC)/vrt_kernels.hip $(HDRS) | $(BLD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BLD)/vrt_sort.o: $(SRC)/vrt_sort.hip $(HDRS) | $(BLD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BLD)/vrt_build.o: $(SRC)/vrt_build.hip $(HDRS) | $(BLD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BLD)/vrt_host.o: $(SRC)/vrt_host.cpp $(HDRS) | $(BLD)
@@ -53,11 +56,11 @@ oracle:
 	$(MAKE) -C oracle
 
 # A/B variant of the kernels:  make variant NAME=v0 DEFS="-DVRT_EXPAND_V=0"
-variant: $(HOSTOBJS) $(BLD)/vrt_sort.o | $(BLD)
+variant: $(HOSTOBJS) $(BLD)/vrt_sort.o $(BLD)/vrt_build.o | $(BLD)
 	mkdir -p build/variants
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
-	  build/variants/k_$(NAME).o $(BLD)/vrt_sort.o $(HOSTOBJS) -lpthread
+	  build/variants/k_$(NAME).o $(BLD)/vrt_sort.o $(BLD)/vrt_build.o $(HOSTOBJS) -lpthread
 
 # ISA listing + register/occupancy report of the kernels (for DESIGN.md)
 isa: | $(BLD)

@@ -88,6 +88,7 @@ typedef struct {
         float root_min[3], root_max[3];
         int64_t device_bytes;
         double build_ms, upload_ms;
+        double build_device_ms;  /* GPU part of a VRT_BUILD_DEVICE build, else 0 */
 } vrt_scene_info_t;
 
 /* Optional per-sample outputs of vrt_render (host arrays, index
@@ -117,12 +118,22 @@ int vrt_device_count(int *n);
  * VRT_E_NODEVICE). */
 int vrt_scene_create(const vrt_scene_desc *desc, int max_depth, int device,
                      vrt_scene **out);
+/* Same, with build flags: VRT_BUILD_DEVICE runs the octree build on the GPU
+ * (level-synchronous SAT descent + hipCUB sorts + BFS flatten, SURVEY §8
+ * f3); the octree is identical to the host build.  Needs device >= 0. */
+#define VRT_BUILD_DEVICE 1
+int vrt_scene_create_ex(const vrt_scene_desc *desc, int max_depth, int device,
+                        int flags, vrt_scene **out);
 void vrt_scene_destroy(vrt_scene *s);
 int vrt_scene_info(const vrt_scene *s, vrt_scene_info_t *info);
 /* Non-empty leaves sorted by voxel id; tris = concatenated leaf lists in
  * insertion (input) order.  Sizes from vrt_scene_info. */
 int vrt_scene_leaves(const vrt_scene *s, uint32_t *voxel, uint32_t *count,
                      int32_t *tris);
+/* The flattened octree, nodes entries each: box (min xyz,
+ * max xyz), word a (first child | 0x80000000 + count for leaves), word b
+ * (content mask | first leaf record).  Any output may be NULL. */
+int vrt_scene_nodes(const vrt_scene *s, float *box, uint32_t *a, uint32_t *b);
 
 /* ---- camera (host, VRT/camera.cc) ------------------------------------ */
 int vrt_camera_init(float fov, const float eye[3], const float spot[3],

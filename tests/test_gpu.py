@@ -349,3 +349,41 @@ def test_trace_device_tiles_reassemble(proxy_small):
     vrt.unpack_tiles_device(film, n, g.data_ptr(), img.data_ptr())
     torch.cuda.synchronize()
     assert np.array_equal(bits(img.cpu().numpy().reshape(40, 48, 3)), bits(direct))
+
+
+# ---- GPU octree build ----
+@pytest.mark.parametrize("depth", [1, 2, 5, 8, 9])
+def test_device_build_equals_host_build(proxy_small, depth):
+    """VRT_BUILD_DEVICE produces the host build's octree array for array:
+    node boxes, child/leaf words, content masks, leaf lists, info."""
+    scenes = [proxy_small, scene_from(golden("scene_soup.npz"))]
+    for sd in scenes:
+        h = vrt.VoxelOctree(sd, depth)
+        g = vrt.VoxelOctree(sd, depth, build_on_device=True)
+        for x, y in zip(h.nodes(), g.nodes()):
+            assert np.array_equal(bits(x), bits(y))
+        for x, y in zip(h.leaves(), g.leaves()):
+            assert np.array_equal(x, y)
+        for f in ("nodes", "internal", "leaves", "nonempty_leaves", "tri_refs"):
+            assert getattr(h.info, f) == getattr(g.info, f), f
+        assert g.info.build_device_ms > 0
+    # and it renders identically
+    mn, mx = g.root_box
+    fov, eye, spot, up = vrt.sweep_pose(mn, mx, 5, 16)
+    cam, film = vrt.Camera(fov, eye, spot, up), vrt.Film(1, 1, 40, 40)
+    assert np.array_equal(bits(h.render(cam, film)), bits(g.render(cam, film)))
+
+
+def test_device_build_edge_scenes():
+    one = vrt.SceneData(np.float32([[0, 0, 0, 1, 0, 0, 0, 1, 0]]), np.float32([[0, 0, 1] * 3]))
+    flat = vrt.SceneData(np.float32([[0, 0, 0, 1, 0, 0, 0, 1, 0], [1, 1, 0, 0, 1, 0, 1, 0, 0]]),
+                         np.tile(np.float32([0, 0, 1]), (2, 3)))
+    empty = vrt.SceneData(np.zeros((0, 9), np.float32), np.zeros((0, 9), np.float32))
+    for sd in (one, flat, empty):
+        for depth in (1, 4, 7, 11):
+            h = vrt.VoxelOctree(sd, depth)
+            g = vrt.VoxelOctree(sd, depth, build_on_device=True)
+            for x, y in zip(h.nodes(), g.nodes()):
+                assert np.array_equal(bits(x), bits(y))
+            for x, y in zip(h.leaves(), g.leaves()):
+                assert np.array_equal(x, y)

@@ -272,3 +272,22 @@ def test_trace_api_host_only_scene():
     assert e.value.status == vrt._ffi.VRT_E_NODEVICE
     with pytest.raises(vrt.VrtError):
         tree.render_trace(cam, vrt.Film(1, 1, 16, 16))
+
+
+def test_scene_nodes_and_build_flags():
+    """vrt_scene_nodes exposes the flattened octree; its structure agrees with
+    the oracle's counts; VRT_BUILD_DEVICE without a device is rejected."""
+    sd = vrt.SceneData.proxy(0.05, 1)
+    tree = vrt.VoxelOctree(sd, 6, device=-1)
+    box, a, b = tree.nodes()
+    info, rbox = po.Scene(sd, 6).info()
+    assert len(a) == info[0]
+    assert np.array_equal(box[0].view(np.uint32), rbox.view(np.uint32))
+    leaf = (a & 0x80000000) != 0
+    assert (~leaf).sum() == info[1] and leaf.sum() == info[2]
+    assert ((a & 0x7FFFFFFF)[leaf] > 0).sum() == info[3]
+    # internal: children block 1 + 8j in order; mask bit c set iff child c has content
+    internal = np.nonzero(~leaf)[0]
+    assert np.array_equal(a[internal], 1 + 8 * np.arange(len(internal)))
+    with pytest.raises(vrt.VrtError):
+        vrt.VoxelOctree(sd, 6, device=-1, build_on_device=True)

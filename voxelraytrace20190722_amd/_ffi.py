@@ -59,7 +59,8 @@ class SceneInfo(C.Structure):
                 ("tri_refs", C.c_int64), ("max_depth", C.c_int32),
                 ("device", C.c_int32), ("root_min", C.c_float * 3),
                 ("root_max", C.c_float * 3), ("device_bytes", C.c_int64),
-                ("build_ms", C.c_double), ("upload_ms", C.c_double)]
+                ("build_ms", C.c_double), ("upload_ms", C.c_double),
+                ("build_device_ms", C.c_double)]
 
 
 class Samples(C.Structure):
@@ -81,14 +82,17 @@ class ObjInfo(C.Structure):
 
 
 VRT_OBJ_PARSE_ONLY = 1
+VRT_BUILD_DEVICE = 1
 
 _P = C.c_void_p
 SIGNATURES = {
     "vrt_device_count": (C.c_int, [i32p]),
     "vrt_scene_create": (C.c_int, [C.POINTER(SceneDesc), C.c_int, C.c_int, C.POINTER(_P)]),
+    "vrt_scene_create_ex": (C.c_int, [C.POINTER(SceneDesc), C.c_int, C.c_int, C.c_int, C.POINTER(_P)]),
     "vrt_scene_destroy": (None, [_P]),
     "vrt_scene_info": (C.c_int, [_P, C.POINTER(SceneInfo)]),
     "vrt_scene_leaves": (C.c_int, [_P, u32p, u32p, i32p]),
+    "vrt_scene_nodes": (C.c_int, [_P, f32p, u32p, u32p]),
     "vrt_camera_init": (C.c_int, [C.c_float, f32p, f32p, f32p, C.c_float, C.c_float,
                                   C.POINTER(Camera)]),
     "vrt_gen_rays4": (C.c_int, [C.POINTER(Camera), C.POINTER(Film), C.c_int, C.c_int,

@@ -277,11 +277,12 @@ class VoxelOctree:
     """The octree built by gi::ray_march_init and resident on one device
     (device < 0: host-only, for inspecting the build)."""
 
-    def __init__(self, scene, max_depth, device=0):
+    def __init__(self, scene, max_depth, device=0, build_on_device=False):
         self.scene = scene  # keeps the arrays alive for the descriptor
         h = C.c_void_p()
         d = scene.desc()
-        check(lib().vrt_scene_create(C.byref(d), int(max_depth), int(device), C.byref(h)),
+        flags = _ffi.VRT_BUILD_DEVICE if build_on_device else 0
+        check(lib().vrt_scene_create_ex(C.byref(d), int(max_depth), int(device), flags, C.byref(h)),
               "vrt_scene_create")
         self.h = h
         self.max_depth = int(max_depth)
@@ -302,6 +303,17 @@ class VoxelOctree:
     @property
     def root_box(self):
         return (np.array(self.info.root_min[:], np.float32), np.array(self.info.root_max[:], np.float32))
+
+    def nodes(self):
+        """The flattened octree as uploaded: (boxes (n,6) f32, word a, word b) per
+        node in BFS child-block order."""
+        n = self.info.nodes
+        box = np.zeros((n, 6), np.float32)
+        a = np.zeros(n, np.uint32)
+        b = np.zeros(n, np.uint32)
+        check(lib().vrt_scene_nodes(self.h, ptr(box, _ffi.f32p), ptr(a, _ffi.u32p), ptr(b, _ffi.u32p)),
+              "vrt_scene_nodes")
+        return box, a, b
 
     def leaves(self):
         """(voxel ids, counts, concatenated triangle lists) of the non-empty leaves."""

@@ -327,7 +327,11 @@ struct vrt_scene {
         std::mutex mu;
 };
 
-static int build_tree(vrt_scene *s, const vrt_scene_desc *d)
+static int finish_tree(vrt_scene *s, const vrt_scene_desc *d, const Box &root, const std::vector<uint64_t> &refs,
+                       int64_t ninternal);
+static int check_device(int device);
+
+static int build_tree(vrt_scene *s, const vrt_scene_desc *d, bool on_device)
 {
         const int D = s->max_depth;
         const int n = d->ntri;
@@ -353,6 +357,21 @@ static int build_tree(vrt_scene *s, const vrt_scene_desc *d)
                 }
         }
 
+        if (on_device) {
+                // level-synchronous descent, sorts, flatten and masks on the GPU
+                DeviceBuild db;
+                std::string err;
+                int rc = check_device(s->device);
+                if (rc)
+                        return rc;
+                if (build_tree_device(s->device, d->pos, n, root.mn, root.mx, D, &db, &err) != hipSuccess)
+                        return fail(VRT_E_DEVICE, "device octree build: %s", err.c_str());
+                s->nodes.swap(db.nodes);
+                s->node_vox.swap(db.node_vox);
+                s->level_begin.swap(db.level_begin);
+                s->info.build_device_ms = db.device_ms;
+                return finish_tree(s, d, root, db.refs, db.ninternal);
+        }
         // parallel per-triangle descent
         unsigned nth = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
         if (n < 4096)
@@ -505,6 +524,15 @@ static int build_tree(vrt_scene *s, const vrt_scene_desc *d)
                         }
                 }
         }
+        return finish_tree(s, d, root, refs, ninternal);
+}
+
+// leaf records with inlined vertices + scene info (both build paths)
+static int finish_tree(vrt_scene *s, const vrt_scene_desc *d, const Box &root, const std::vector<uint64_t> &refs,
+                       int64_t ninternal)
+{
+        const int64_t nnodes = (int64_t)s->nodes.size();
+        s->refs.resize(refs.size());
         for (size_t i = 0; i < refs.size(); ++i) {
                 const uint32_t t = (uint32_t)(refs[i] & 0xFFFFFFFFu);
                 RefRec &rr = s->refs[i];
@@ -655,12 +683,22 @@ static int validate_desc(const vrt_scene_desc *d, int max_depth)
 extern "C" int vrt_scene_create(const vrt_scene_desc *d, int max_depth,
                                 int device, vrt_scene **out)
 {
+        return vrt_scene_create_ex(d, max_depth, device, 0, out);
+}
+
+extern "C" int vrt_scene_create_ex(const vrt_scene_desc *d, int max_depth,
+                                   int device, int flags, vrt_scene **out)
+{
         if (!out)
                 return fail(VRT_E_INVALID, "null out");
         *out = nullptr;
         int rc = validate_desc(d, max_depth);
         if (rc)
                 return rc;
+        if (flags & ~VRT_BUILD_DEVICE)
+                return fail(VRT_E_INVALID, "unknown flags %#x", flags);
+        if ((flags & VRT_BUILD_DEVICE) && device < 0)
+                return fail(VRT_E_INVALID, "VRT_BUILD_DEVICE needs a device (device >= 0)");
         std::unique_ptr<vrt_scene> s(new (std::nothrow) vrt_scene);
         if (!s)
                 return fail(VRT_E_NOMEM, "scene alloc");
@@ -669,7 +707,7 @@ extern "C" int vrt_scene_create(const vrt_scene_desc *d, int max_depth,
         s->ntri = d->ntri;
         const double t0 = now_ms();
         try {
-                rc = build_tree(s.get(), d);
+                rc = build_tree(s.get(), d, (flags & VRT_BUILD_DEVICE) != 0);
                 if (rc)
                         return rc;
                 const int n = d->ntri;
@@ -756,6 +794,24 @@ extern "C" int vrt_scene_info(const vrt_scene *s, vrt_scene_info_t *info)
         if (!s || !info)
                 return fail(VRT_E_INVALID, "null argument");
         *info = s->info;
+        return VRT_OK;
+}
+
+extern "C" int vrt_scene_nodes(const vrt_scene *s, float *box, uint32_t *a, uint32_t *b)
+{
+        if (!s)
+                return fail(VRT_E_INVALID, "null argument");
+        for (size_t i = 0; i < s->nodes.size(); ++i) {
+                const NodeRec &nr = s->nodes[i];
+                if (box) {
+                        std::memcpy(box + 6 * i, nr.bmin, 12);
+                        std::memcpy(box + 6 * i + 3, nr.bmax, 12);
+                }
+                if (a)
+                        a[i] = nr.a;
+                if (b)
+                        b[i] = nr.b;
+        }
         return VRT_OK;
 }
 

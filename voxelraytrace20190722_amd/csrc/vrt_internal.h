@@ -5,6 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+#include <vector>
+
 #include "vrt_math.h"
 
 namespace vrt {
@@ -133,6 +136,19 @@ struct TraceParams {
         float mindist, maxdist;
         float split_up[64];
 };
+
+// GPU octree build (vrt_build.hip): the host build's
+// arrays, produced on `device` and copied back.
+struct DeviceBuild {
+        std::vector<NodeRec> nodes;        // content masks included
+        std::vector<uint32_t> node_vox;
+        std::vector<uint64_t> refs;        // sorted (leaf code << 32 | tri)
+        std::vector<int64_t> level_begin;  // BFS level ranges (+ end)
+        int64_t ninternal = 0;
+        double device_ms = 0;              // descent + sorts + flatten + masks
+};
+hipError_t build_tree_device(int device, const float *pos, int ntri, const float root_mn[3],
+                             const float root_mx[3], int max_depth, DeviceBuild *out, std::string *err);
 
 // Kernel launchers (vrt_kernels.hip)
 hipError_t launch_render(const RenderParams &p, bool instrumented,
