@@ -375,13 +375,13 @@ def test_device_build_equals_host_build(proxy_small, depth):
 
 
 def test_device_build_edge_scenes():
-    one = vrt.SceneData(np.float32([[0, 0, 0, 1, 0, 0, 0, 1, 0]]), np.float32([[0, 0, 1] * 3]))
+    one = vrt.SceneData(np.float32([[0, 0, 0, 1, 0, 0.5, 0, 1, 1]]), np.float32([[0, 0, 1] * 3]))
     flat = vrt.SceneData(np.float32([[0, 0, 0, 1, 0, 0, 0, 1, 0], [1, 1, 0, 0, 1, 0, 1, 0, 0]]),
                          np.tile(np.float32([0, 0, 1]), (2, 3)))
     empty = vrt.SceneData(np.zeros((0, 9), np.float32), np.zeros((0, 9), np.float32))
     # a zero-thickness scene splits into all 8 children at every level (both
     # z halves of a flat box coincide): 8^(depth-1) leaves, so keep it shallow
-    for sd, depths in ((one, (1, 4, 8)), (flat, (1, 3, 5)), (empty, (1, 11))):
+    for sd, depths in ((one, (1, 4, 9)), (flat, (1, 3, 5)), (empty, (1, 11))):
         for depth in depths:
             h = vrt.VoxelOctree(sd, depth)
             g = vrt.VoxelOctree(sd, depth, build_on_device=True)
