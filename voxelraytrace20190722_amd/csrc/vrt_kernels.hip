@@ -386,7 +386,7 @@ __device__ __forceinline__ bool leaf_isect_v1(const RefRec *__restrict__ refs,
 
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).
-template <bool kCount, bool kFast>
+template <bool kCount, bool kFast, int kS = kBlock>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint32_t *stk_base,
                                           uint32_t *stk_ord,
@@ -434,12 +434,12 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                 if (sp == 0)
                                         break;
                                 --sp;
-                                base = stk_base[sp * kBlock];
-                                const uint32_t w = stk_ord[sp * kBlock];
+                                base = stk_base[sp * kS];
+                                const uint32_t w = stk_ord[sp * kS];
                                 order = w & 0xFFFFFFu;
                                 cnt = (int)(w >> 24);
                                 if (kCount) {
-                                        const uint32_t x = stk_aux[sp * kBlock];
+                                        const uint32_t x = stk_aux[sp * kS];
                                         fpos = x & 0xFFFFFFu;
                                         depth = x >> 24;
                                 }
@@ -450,14 +450,14 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         --cnt;
                         node = base + ci;
                         if (kCount)
-                                path_rem[depth * kBlock] = 7u - ((fpos >> (3 * ci)) & 7u);
+                                path_rem[depth * kS] = 7u - ((fpos >> (3 * ci)) & 7u);
                         load_node(sc.nodes, node, bmin, bmax, a, b);
                         if (!(a & kLeafBit)) {
                                 if (cnt) {
-                                        stk_base[sp * kBlock] = base;
-                                        stk_ord[sp * kBlock] = order | ((uint32_t)cnt << 24);
+                                        stk_base[sp * kS] = base;
+                                        stk_ord[sp * kS] = order | ((uint32_t)cnt << 24);
                                         if (kCount)
-                                                stk_aux[sp * kBlock] = fpos | (depth << 24);
+                                                stk_aux[sp * kS] = fpos | (depth << 24);
                                         ++sp;
                                 }
                                 order = expand<kCount, kFast>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
@@ -488,12 +488,12 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         if (sp == 0)
                                 break;
                         --sp;
-                        base = stk_base[sp * kBlock];
-                        const uint32_t w = stk_ord[sp * kBlock];
+                        base = stk_base[sp * kS];
+                        const uint32_t w = stk_ord[sp * kS];
                         order = w & 0xFFFFFFu;
                         cnt = (int)(w >> 24);
                         if (kCount) {
-                                const uint32_t x = stk_aux[sp * kBlock];
+                                const uint32_t x = stk_aux[sp * kS];
                                 fpos = x & 0xFFFFFFu;
                                 depth = x >> 24;
                         }
@@ -504,14 +504,14 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 --cnt;
                 const uint32_t node = base + ci;
                 if (kCount)
-                        path_rem[depth * kBlock] = 7u - ((fpos >> (3 * ci)) & 7u);
+                        path_rem[depth * kS] = 7u - ((fpos >> (3 * ci)) & 7u);
                 load_node(sc.nodes, node, bmin, bmax, a, b);
                 if (!(a & kLeafBit)) {
                         if (cnt) {
-                                stk_base[sp * kBlock] = base;
-                                stk_ord[sp * kBlock] = order | ((uint32_t)cnt << 24);
+                                stk_base[sp * kS] = base;
+                                stk_ord[sp * kS] = order | ((uint32_t)cnt << 24);
                                 if (kCount)
-                                        stk_aux[sp * kBlock] = fpos | (depth << 24);
+                                        stk_aux[sp * kS] = fpos | (depth << 24);
                                 ++sp;
                         }
                         order = expand<kCount, kFast>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
@@ -536,7 +536,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 uint32_t A = 1 + 8 * nexp;
                 if (m.hit)
                         for (uint32_t lv = 1; lv <= depth; ++lv)
-                                A -= path_rem[lv * kBlock];
+                                A -= path_rem[lv * kS];
                 m.A = A;
         }
 }
@@ -566,16 +566,16 @@ __device__ __forceinline__ bool fast_ok(const RayK &r)
         return ok;
 }
 
-template <bool kCount>
+template <bool kCount, int kS = kBlock>
 __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const RayK &r,
                                                    uint32_t *sb, uint32_t *so,
                                                    uint32_t *sa, uint32_t *pr,
                                                    MarchResult &m)
 {
         if (__all(sc.fast_ok && fast_ok(r)))
-                ray_march<kCount, true>(sc, r, sb, so, sa, pr, m);
+                ray_march<kCount, true, kS>(sc, r, sb, so, sa, pr, m);
         else
-                ray_march<kCount, false>(sc, r, sb, so, sa, pr, m);
+                ray_march<kCount, false, kS>(sc, r, sb, so, sa, pr, m);
 }
 
 // Triangle::get_albedo (VRT/voxel_octree.cc:472-484) with Triangle::isect's
@@ -633,38 +633,48 @@ __device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
 }
 
 // ---------------------------------------------------------------------------
-// Primary render: one workgroup per 8x8 tile.
+// Primary render: an 8x8 tile = 4 waves of 4x4 pixels x 4 samples, run as
+// VRT_RENDER_WAVES waves per workgroup (4: one workgroup per tile; 1: one
+// wave per workgroup, so a finished wave frees its slot and LDS at once).
 // ---------------------------------------------------------------------------
+#ifndef VRT_RENDER_WAVES
+#define VRT_RENDER_WAVES 1
+#endif
+constexpr int kRenderBlock = 64 * VRT_RENDER_WAVES;
 template <bool kCount>
 #ifndef VRT_WAVES_PER_EU
 // 6 waves per SIMD (80 VGPRs, a 32-B/lane spill) measured 8% faster than
 // the unconstrained 4 waves/SIMD (99 VGPRs): the march is latency-bound.
 #define VRT_WAVES_PER_EU 6
 #endif
-__global__ __launch_bounds__(kBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k_render(RenderParams p)
+__global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k_render(RenderParams p)
 {
-        __shared__ uint32_t stk_base[kStack * kBlock];
-        __shared__ uint32_t stk_ord[kStack * kBlock];
-        __shared__ uint32_t stk_aux[kCount ? kStack * kBlock : 1];
-        __shared__ uint32_t path_rem[kCount ? (kStack + 1) * kBlock : 1];
+        constexpr int kB = kRenderBlock;
+        __shared__ uint32_t stk_base[kStack * kB];
+        __shared__ uint32_t stk_ord[kStack * kB];
+        __shared__ uint32_t stk_aux[kCount ? kStack * kB : 1];
+        __shared__ uint32_t path_rem[kCount ? (kStack + 1) * kB : 1];
 
         const int tid = threadIdx.x;
-        // XCD-aware tile order: blocks b, b+8, ... run on one XCD; give them
-        // consecutive tiles so each XCD's L2 serves one screen region.
+        // XCD-aware order: blocks b, b+8, ... run on one XCD; give them
+        // consecutive work units (a unit = kUnitsPerTile-th of an 8x8 tile)
+        // so each XCD's L2 serves one screen region.
+        constexpr int kQ = 4 / VRT_RENDER_WAVES;  // units per tile
         const int nb = gridDim.x;
         const int b = blockIdx.x;
         const int per = (nb + 7) >> 3;
         const int xcd = b & 7, slot = b >> 3;
-        int k = xcd * per + slot;
+        int u = xcd * per + slot;
         if ((nb & 7) != 0) {
                 // uneven grid: fall back to the identity map
-                k = b;
+                u = b;
         }
-        if (k >= p.tiles_this_rank)
+        if (u >= p.tiles_this_rank * kQ)
                 return;
+        const int k = u / kQ;
         const int t = p.rank + k * p.nranks;
         const int tx = t % p.ntx, ty = t / p.ntx;
-        const int wave = tid >> 6, lane = tid & 63;
+        const int wave = (u % kQ) * VRT_RENDER_WAVES + (tid >> 6), lane = tid & 63;
         const int s = lane & 3, pix = lane >> 2;
         const int lx = (wave & 1) * 4 + (pix & 3);
         const int ly = (wave >> 1) * 4 + (pix >> 2);
@@ -678,9 +688,9 @@ __global__ __launch_bounds__(kBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k_rende
                                  dn, c.tmin, c.tmax);
 
         MarchResult m;
-        ray_march_dispatch<kCount>(p.sc, r, stk_base + tid, stk_ord + tid,
-                          stk_aux + (kCount ? tid : 0),
-                          path_rem + (kCount ? tid : 0), m);
+        ray_march_dispatch<kCount, kB>(p.sc, r, stk_base + tid, stk_ord + tid,
+                                       stk_aux + (kCount ? tid : 0),
+                                       path_rem + (kCount ? tid : 0), m);
 
         f3 col;
         if (m.hit) {
@@ -1020,11 +1030,11 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
         if (p.tiles_this_rank <= 0)
                 return hipSuccess;
         // round the grid up to a multiple of 8 (one slot per XCD)
-        const int grid = (p.tiles_this_rank + 7) & ~7;
+        const int grid = (p.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
         if (instrumented)
-                hipLaunchKernelGGL(k_render<true>, dim3(grid), dim3(kBlock), 0, st, p);
+                hipLaunchKernelGGL(k_render<true>, dim3(grid), dim3(kRenderBlock), 0, st, p);
         else
-                hipLaunchKernelGGL(k_render<false>, dim3(grid), dim3(kBlock), 0, st, p);
+                hipLaunchKernelGGL(k_render<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
         return hipGetLastError();
 }
 
@@ -1126,14 +1136,16 @@ __device__ __forceinline__ f3 illum_dir(int i)
 __device__ __forceinline__ bool tile_lane(const RenderParams &p, int &k, int &px, int &py,
                                           int &s, int &lx, int &ly)
 {
+        constexpr int kQ = 4 / VRT_RENDER_WAVES;  // work units per tile
         const int nb = gridDim.x, b = blockIdx.x;
         const int per = (nb + 7) >> 3;
-        k = ((nb & 7) != 0) ? b : (b & 7) * per + (b >> 3);
-        if (k >= p.tiles_this_rank)
+        const int u = ((nb & 7) != 0) ? b : (b & 7) * per + (b >> 3);
+        if (u >= p.tiles_this_rank * kQ)
                 return false;
+        k = u / kQ;
         const int t = p.rank + k * p.nranks;
         const int tx = t % p.ntx, ty = t / p.ntx;
-        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        const int tid = threadIdx.x, wave = (u % kQ) * VRT_RENDER_WAVES + (tid >> 6), lane = tid & 63;
         s = lane & 3;
         const int pix = lane >> 2;
         lx = (wave & 1) * 4 + (pix & 3);
@@ -1143,10 +1155,10 @@ __device__ __forceinline__ bool tile_lane(const RenderParams &p, int &k, int &px
         return true;
 }
 
-__global__ __launch_bounds__(kBlock) void k_light(LightParams p)
+__global__ __launch_bounds__(kRenderBlock) void k_light(LightParams p)
 {
-        __shared__ uint32_t stk_base[kStack * kBlock];
-        __shared__ uint32_t stk_ord[kStack * kBlock];
+        __shared__ uint32_t stk_base[kStack * kRenderBlock];
+        __shared__ uint32_t stk_ord[kStack * kRenderBlock];
         const int tid = threadIdx.x;
         int k, px, py, s, lx, ly;
         if (!tile_lane(p.r, k, px, py, s, lx, ly))
@@ -1157,7 +1169,7 @@ __global__ __launch_bounds__(kBlock) void k_light(LightParams p)
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false>(p.r.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
         // canonical order: render_mt task t = tx*8 + ty (VRT/camera.h:50-56)
         const int tx = px / p.ptx, ty = py / p.pty;
         const int64_t task = (int64_t)tx * 8 + ty;
@@ -1385,10 +1397,10 @@ __device__ __forceinline__ f3 cone_trace_isect(const TraceParams &p, f3 hit, f3 
 
 // trace(root, ray, 5, true) per sample + Film::add(c * .25f)
 // (VRT/main.cc:10-30, 118-123)
-__global__ __launch_bounds__(kBlock) void k_trace(TraceParams p)
+__global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
 {
-        __shared__ uint32_t stk_base[kStack * kBlock];
-        __shared__ uint32_t stk_ord[kStack * kBlock];
+        __shared__ uint32_t stk_base[kStack * kRenderBlock];
+        __shared__ uint32_t stk_ord[kStack * kRenderBlock];
         const int tid = threadIdx.x, lane = tid & 63;
         int k, px, py, s, lx, ly;
         if (!tile_lane(p.r, k, px, py, s, lx, ly))
@@ -1399,7 +1411,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceParams p)
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false>(p.r.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
         f3 col;
         if (m.hit) {
                 f3 nrm;
@@ -1451,8 +1463,8 @@ hipError_t launch_light(const LightParams &p, hipStream_t st)
 {
         if (p.r.tiles_this_rank <= 0)
                 return hipSuccess;
-        const int grid = (p.r.tiles_this_rank + 7) & ~7;
-        hipLaunchKernelGGL(k_light, dim3(grid), dim3(kBlock), 0, st, p);
+        const int grid = (p.r.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
+        hipLaunchKernelGGL(k_light, dim3(grid), dim3(kRenderBlock), 0, st, p);
         return hipGetLastError();
 }
 
@@ -1495,8 +1507,8 @@ hipError_t launch_trace(const TraceParams &p, hipStream_t st)
 {
         if (p.r.tiles_this_rank <= 0)
                 return hipSuccess;
-        const int grid = (p.r.tiles_this_rank + 7) & ~7;
-        hipLaunchKernelGGL(k_trace, dim3(grid), dim3(kBlock), 0, st, p);
+        const int grid = (p.r.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
+        hipLaunchKernelGGL(k_trace, dim3(grid), dim3(kRenderBlock), 0, st, p);
         return hipGetLastError();
 }
 
