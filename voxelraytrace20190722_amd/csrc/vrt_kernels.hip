@@ -49,7 +49,7 @@ __device__ __forceinline__ void load_node(const NodeRec *__restrict__ nodes,
 }
 
 #ifndef VRT_EXPAND_V
-#define VRT_EXPAND_V 1
+#define VRT_EXPAND_V 2
 #endif
 
 // Expand an internal node with box [bmin,bmax]: slab-test its 8 children
@@ -165,6 +165,107 @@ __device__ __forceinline__ uint32_t expand_v1(const float bmin[3],
         return order;
 }
 
+// v2 (fast path, uninstrumented): the same slab tests as v1, but the hit
+// children -- at most 4 for a line through 8 octants, save degenerate
+// boxes -- are ordered by a 4-slot sorting network on the total order
+// (dist, child index), which is exactly the stable order v1's ranks and
+// libstdc++'s insertion sort produce (strict <, ties by index; no dist is
+// NaN on the fast path).  A wave with any lane at > 4 hit children takes
+// v1's rank path.
+__device__ __forceinline__ void ce4(float &da, uint32_t &ia, float &db, uint32_t &ib)
+{
+        const bool sw = (db < da) | ((db == da) & (ib < ia));
+        const float td = da;
+        const uint32_t ti = ia;
+        da = sw ? db : da;
+        ia = sw ? ib : ia;
+        db = sw ? td : db;
+        ib = sw ? ti : ib;
+}
+
+__device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float bmax[3], const RayK &r, int &cnt,
+                                              uint32_t content)
+{
+        const float oo[3] = { r.o.x, r.o.y, r.o.z };
+        const float dd[3] = { r.d.x, r.d.y, r.d.z };
+        const float di[3] = { r.dinv.x, r.dinv.y, r.dinv.z };
+        float nr[3][2], fr[3][2], q[3][2];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+                const float h = (bmax[k] - bmin[k]) / 2.0f;
+                const float a0 = bmin[k];
+                const float b = bmin[k] + h;
+                const float c = b + h;
+                const float ta = (a0 - oo[k]) * di[k];
+                const float tb = (b - oo[k]) * di[k];
+                const float tc = (c - oo[k]) * di[k];
+                nr[k][0] = fminf(ta, tb);
+                fr[k][0] = fmaxf(ta, tb);
+                nr[k][1] = fminf(tb, tc);
+                fr[k][1] = fmaxf(tb, tc);
+                q[k][0] = dd[k] * ((a0 + b) * .5f - oo[k]);
+                q[k][1] = dd[k] * ((b + c) * .5f - oo[k]);
+        }
+        const float qx0 = 0.0f + q[0][0], qx1 = 0.0f + q[0][1];
+        uint32_t hm = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+                const int mx = (i >> 2) & 1, my = (i >> 1) & 1, mz = i & 1;
+                const float t0 = fmaxf(fmaxf(nr[0][mx], nr[1][my]), nr[2][mz]);
+                const float t1 = fminf(fminf(fr[0][mx], fr[1][my]), fr[2][mz]);
+                const bool h = ((content >> i) & 1u) & !(t0 > t1) &
+                               (((t0 >= r.tmin) & (t0 <= r.tmax)) | ((t1 >= r.tmin) & (t1 <= r.tmax)));
+                hm |= (uint32_t)h << i;
+        }
+        const int n = __popc(hm);
+        cnt = n;
+        if (__any(n > 4)) {
+                // rare: v1's full rank order over the same mask
+                float dist[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                        const int mx = (i >> 2) & 1, my = (i >> 1) & 1, mz = i & 1;
+                        dist[i] = ((mx ? qx1 : qx0) + q[1][my]) + q[2][mz];
+                }
+                uint32_t rk[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                        rk[i] = 0;
+#pragma unroll
+                for (int i = 1; i < 8; ++i)
+#pragma unroll
+                        for (int j = 0; j < i; ++j) {
+                                const bool c = dist[i] < dist[j];
+                                rk[j] += (uint32_t)(c & ((hm >> i) & 1u));
+                                rk[i] += (uint32_t)(!c & ((hm >> j) & 1u));
+                        }
+                uint32_t order = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                        order |= ((hm >> i) & 1u) ? ((uint32_t)i << (3 * rk[i])) : 0u;
+                return order;
+        }
+        // up to 4 hit children into slots in index order; empty slots sort last
+        float d[4];
+        uint32_t id[4];
+        uint32_t m = hm;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+                const uint32_t i = m ? (uint32_t)__builtin_ctz(m) : 8u;
+                m &= m - 1u;
+                const uint32_t mx = (i >> 2) & 1u, my = (i >> 1) & 1u, mz = i & 1u;
+                const float dv = ((mx ? qx1 : qx0) + (my ? q[1][1] : q[1][0])) + (mz ? q[2][1] : q[2][0]);
+                d[k] = i < 8u ? dv : __int_as_float(0x7f800000);
+                id[k] = i;
+        }
+        ce4(d[0], id[0], d[1], id[1]);
+        ce4(d[2], id[2], d[3], id[3]);
+        ce4(d[0], id[0], d[2], id[2]);
+        ce4(d[1], id[1], d[3], id[3]);
+        ce4(d[1], id[1], d[2], id[2]);
+        return (id[0] & 7u) | ((id[1] & 7u) << 3) | ((id[2] & 7u) << 6) | ((id[3] & 7u) << 9);
+}
+
 template <bool kFullPos>
 __device__ __forceinline__ uint32_t expand_v0(const float bmin[3],
                                            const float bmax[3],
@@ -245,6 +346,10 @@ __device__ __forceinline__ uint32_t expand(const float bmin[3],
 {
 #if VRT_EXPAND_V == 0
         return expand_v0<kFullPos>(bmin, bmax, r, cnt, full_pos);
+#elif VRT_EXPAND_V == 2
+        if (kFast && !kFullPos)
+                return expand_v2(bmin, bmax, r, cnt, content);
+        return expand_v1<kFullPos, kFast>(bmin, bmax, r, cnt, full_pos, content);
 #else
         return expand_v1<kFullPos, kFast>(bmin, bmax, r, cnt, full_pos, content);
 #endif
