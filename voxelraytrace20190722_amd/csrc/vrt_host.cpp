@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -318,6 +319,8 @@ struct vrt_scene {
         bool lm_ready = false;
         void *d_light = nullptr;
         size_t light_bytes = 0;
+        void *d_trace = nullptr;  // split-trace scratch (records + colours)
+        size_t trace_bytes = 0;
         // device
         void *d_mem = nullptr;
         DevScene dev{};
@@ -769,7 +772,7 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
 {
         if (!s)
                 return;
-        if (s->d_mem || s->d_lm || s->d_light || s->stream || s->ev0 || s->ev1) {
+        if (s->d_mem || s->d_lm || s->d_light || s->d_trace || s->stream || s->ev0 || s->ev1) {
                 (void)hipSetDevice(s->device);
                 if (s->stream)
                         (void)hipStreamSynchronize(s->stream);
@@ -779,6 +782,8 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                         (void)hipFree(s->d_lm);
                 if (s->d_light)
                         (void)hipFree(s->d_light);
+                if (s->d_trace)
+                        (void)hipFree(s->d_trace);
                 if (s->ev0)
                         (void)hipEventDestroy(s->ev0);
                 if (s->ev1)
@@ -1213,9 +1218,14 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         const int64_t ns = (int64_t)64 * ptx * pty * 4;
         if (ns > 0x7FFFFFFF)
                 return fail(VRT_E_INVALID, "light film too large (%lld samples)", (long long)ns);
+        // one block: light map, cone-descent records, finiteness flag
         if (!s->d_lm)
-                HIPCHK(hipMalloc(reinterpret_cast<void **>(&s->d_lm), (size_t)nnodes * sizeof(LMRec)));
+                HIPCHK(hipMalloc(reinterpret_cast<void **>(&s->d_lm),
+                                 (size_t)nnodes * (sizeof(LMRec) + sizeof(float4)) + 256));
+        float4 *d_cc = reinterpret_cast<float4 *>(s->d_lm + nnodes);
+        uint32_t *d_bad = reinterpret_cast<uint32_t *>(d_cc + nnodes);
         HIPCHK(hipMemsetAsync(s->d_lm, 0, (size_t)nnodes * sizeof(LMRec), s->stream));
+        HIPCHK(hipMemsetAsync(d_bad, 0, 4, s->stream));
         // scratch: keys/vals in+out, per-sample (illum, normal), sort temp
         size_t sort_bytes = 0;
         const uint32_t miss_key = (uint32_t)nnodes;
@@ -1261,6 +1271,7 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         const int nlev = (int)s->level_begin.size() - 1;
         for (int l = nlev; l >= 1; --l)
                 HIPCHK(launch_lm_level(s->dev.nodes, s->level_begin[l - 1], s->level_begin[l], s->d_lm, s->stream));
+        HIPCHK(launch_lm_aux(s->dev.nodes, s->d_lm, nnodes, d_cc, d_bad, s->stream));
         HIPCHK(hipEventRecord(s->ev1, s->stream));
         s->timed = true;
         unsigned long long h = 0;
@@ -1309,6 +1320,41 @@ static int trace_ok(vrt_scene *s, float min_voxel)
         return VRT_OK;
 }
 
+// Split trace (primary pass -> one lane per cone -> film add) unless
+// VRT_TRACE_FUSED=1 selects the single fused kernel (A/B and tests).
+static bool trace_fused()
+{
+        static const bool f = [] {
+                const char *e = std::getenv("VRT_TRACE_FUSED");
+                return e && e[0] == '1';
+        }();
+        return f;
+}
+
+static int trace_scratch(vrt_scene *s, const TraceParams &tp, TraceParams *out, hipStream_t st)
+{
+        *out = tp;
+        if (trace_fused())
+                return VRT_OK;
+        const size_t nslots = (size_t)tp.r.tiles_this_rank * 256;
+        const size_t need = nslots * 64 + nslots * 72 + 512;  // records + 6 cone results
+        if (s->trace_bytes < need) {
+                if (s->d_trace) {
+                        HIPCHK(hipDeviceSynchronize());  // callers may have queued work on any stream
+                        (void)hipFree(s->d_trace);
+                        s->d_trace = nullptr;
+                        s->trace_bytes = 0;
+                }
+                HIPCHK(hipMalloc(&s->d_trace, need));
+                s->trace_bytes = need;
+        }
+        (void)st;
+        char *base = static_cast<char *>(s->d_trace);
+        out->rec = reinterpret_cast<float4 *>(base);
+        out->col = reinterpret_cast<float *>(base + ((nslots * 64 + 255) & ~(size_t)255));
+        return VRT_OK;
+}
+
 static void fill_trace_params(vrt_scene *s, const vrt_camera *cam, const vrt_film *film, float min_voxel,
                               int rank, int nranks, TraceParams *tp)
 {
@@ -1317,6 +1363,8 @@ static void fill_trace_params(vrt_scene *s, const vrt_camera *cam, const vrt_fil
         if (!(min_voxel > 0.f))
                 vrt_scene_min_voxel(s, 0, &min_voxel);
         tp->lm = s->d_lm;
+        tp->cc = reinterpret_cast<const float4 *>(s->d_lm + s->nodes.size());
+        tp->lm_bad = reinterpret_cast<const uint32_t *>(tp->cc + s->nodes.size());
         // float mindist = 1.414f * min_voxel_size; maxdist = length(root.aabb.size())
         tp->mindist = 1.414f * min_voxel;
         const f3 sz = mk3(s->info.root_max[0] - s->info.root_min[0], s->info.root_max[1] - s->info.root_min[1],
@@ -1344,11 +1392,13 @@ extern "C" int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam, cons
         if (int rc = trace_ok(s, min_voxel))
                 return rc;
         HIPCHK(hipSetDevice(s->device));
-        TraceParams tp;
-        fill_trace_params(s, cam, film, min_voxel, rank, nranks, &tp);
-        tp.r.image_layout = image_layout;
-        tp.r.out = d_out;
+        TraceParams tp0, tp;
+        fill_trace_params(s, cam, film, min_voxel, rank, nranks, &tp0);
+        tp0.r.image_layout = image_layout;
+        tp0.r.out = d_out;
         hipStream_t st = static_cast<hipStream_t>(stream);
+        if (int rc = trace_scratch(s, tp0, &tp, st))
+                return rc;
         HIPCHK(hipEventRecord(s->ev0, st));
         HIPCHK(launch_trace(tp, st));
         HIPCHK(hipEventRecord(s->ev1, st));
@@ -1375,10 +1425,12 @@ extern "C" int vrt_render_trace(vrt_scene *s, const vrt_camera *cam, const vrt_f
         DevBuf img, dh, dr;
         HIPCHK(hipMalloc(&img.p, npix * 12));
         HIPCHK(hipMemsetAsync(img.p, 0, npix * 12, s->stream));
-        TraceParams tp;
-        fill_trace_params(s, cam, film, min_voxel, 0, 1, &tp);
-        tp.r.image_layout = 1;
-        tp.r.out = static_cast<float *>(img.p);
+        TraceParams tp0, tp;
+        fill_trace_params(s, cam, film, min_voxel, 0, 1, &tp0);
+        tp0.r.image_layout = 1;
+        tp0.r.out = static_cast<float *>(img.p);
+        if (int rc = trace_scratch(s, tp0, &tp, s->stream))
+                return rc;
         if (s_hit) {
                 HIPCHK(hipMalloc(&dh.p, ns * 4));
                 HIPCHK(hipMemsetAsync(dh.p, 0, ns * 4, s->stream));

@@ -133,8 +133,16 @@ struct LightParams {
 struct TraceParams {
         RenderParams r;
         const LMRec *lm;
+        const float4 *cc;          // per node: box centre xyz, word a (cone descent)
+        const uint32_t *lm_bad;    // != 0: some illum is not finite (exact slow path)
         float mindist, maxdist;
         float split_up[64];
+        // split path (rec != nullptr): per-sample records of the primary
+        // pass (4 x float4: hit point | hit flag, normal, albedo or sky,
+        // direct light) and the 6 cone results per sample (col[cone][slot]),
+        // tiles_this_rank*256 slots
+        float4 *rec;
+        float *col;
 };
 
 // GPU octree build (vrt_build.hip): the host build's
@@ -171,6 +179,9 @@ hipError_t launch_lm_accum(int64_t n, const uint32_t *keys_sorted, const uint32_
 hipError_t launch_lm_leaves(const NodeRec *nodes, int64_t nnodes, LMRec *lm, hipStream_t st);
 hipError_t launch_lm_level(const NodeRec *nodes, int64_t begin, int64_t end, LMRec *lm, hipStream_t st);
 hipError_t launch_trace(const TraceParams &p, hipStream_t st);
+// per-node cone-descent records and the light map's finiteness flag
+hipError_t launch_lm_aux(const NodeRec *nodes, const LMRec *lm, int64_t n, float4 *cc, uint32_t *bad,
+                         hipStream_t st);
 // stable radix sort of (key, value) pairs on the low `bits` key bits
 // (vrt_sort.hip); temp == nullptr queries *temp_bytes
 hipError_t sort_pairs_u32(void *temp, size_t *temp_bytes, const uint32_t *keys_in, uint32_t *keys_out,

@@ -1427,8 +1427,95 @@ __device__ __forceinline__ int split_level_of(float x, const float *up)
         return x >= up[e] ? e + 1 : e;
 }
 
+// Cone-descent record per node (box centre as AABB3D::center computes it,
+// child word) and a flag raised when any light-map value is not finite.
+__global__ __launch_bounds__(256) void k_lm_aux(const NodeRec *__restrict__ nodes, const LMRec *__restrict__ lm,
+                                                int64_t n, float4 *__restrict__ cc, uint32_t *bad)
+{
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= n)
+                return;
+        const NodeRec nr = nodes[i];
+        cc[i] = make_float4((nr.bmin[0] + nr.bmax[0]) * .5f, (nr.bmin[1] + nr.bmax[1]) * .5f,
+                            (nr.bmin[2] + nr.bmax[2]) * .5f, __uint_as_float(nr.a));
+        bool ok = __builtin_isfinite(lm[i].cov);
+#pragma unroll
+        for (int f = 0; f < 18; ++f)
+                ok = ok && __builtin_isfinite(lm[i].illum[f]);
+        if (!ok)
+                atomicOr(bad, 1u);
+}
+
+// Fast cone march (finite light map): the same values as cone_march_ref.
+// Two exact shortcuts: a node with coverage +0 adds w * illum = +-0 to the
+// running sum (w = ... * cov) and transparency * 0 to the opacity, which
+// leave them unchanged (the sums start at +0 and never become -0), so its
+// illum is not read; and compute_illum's terms with coefficient +0 are +-0
+// for finite illum and are skipped the same way.  Descent reads 16-B
+// centre/child records.
+__device__ __forceinline__ f3 cone_march_fast(const TraceParams &p, f3 o, f3 d)
+{
+        const float aperture = 0.577350269f, step = .1f, decay = 1.f;
+        const f3 nd = -d;
+        float co[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+                co[i] = clampf(dot(illum_dir(i), nd), 0.f, 1.f);
+        float dist = p.mindist;
+        float opacity = 0.f;
+        f3 diffuse = mk3(0.f, 0.f, 0.f);
+        for (int guard = 0; dist < p.maxdist && opacity < 1.f && guard < (1 << 16); ++guard) {
+                const f3 pt = o + d * dist;
+                const float diam = std_max(p.mindist, aperture * 2.f * dist);
+                if (p.maxdist < diam)
+                        break;
+                int split = split_level_of(p.maxdist / diam, p.split_up);
+                uint32_t ni = 0;
+                float4 c = p.cc[0];
+                uint32_t a = __float_as_uint(c.w);
+                while (!(a & kLeafBit) && split) {
+                        int i = 0;
+                        i += (pt.x > c.x ? 4 : 0);
+                        i += (pt.y > c.y ? 2 : 0);
+                        i += (pt.z > c.z ? 1 : 0);
+                        ni = a + (uint32_t)i;
+                        c = p.cc[ni];
+                        a = __float_as_uint(c.w);
+                        split--;
+                }
+                if (split == 0) {
+                        const float cov = p.lm[ni].cov;
+                        if (cov != 0.f) {
+                                const float *L = p.lm[ni].illum;
+                                f3 il = mk3(0.f, 0.f, 0.f);
+#pragma unroll
+                                for (int i = 0; i < 6; ++i)
+                                        if (co[i] != 0.f)
+                                                il = mk3(il.x + co[i] * L[3 * i + 0], il.y + co[i] * L[3 * i + 1],
+                                                         il.z + co[i] * L[3 * i + 2]);
+                                const float transparency = clampf(1.f - opacity, 0.f, 1.f);
+                                const float aa = cov * step;
+                                const float w = (1.f / (1.f + decay * dist)) * transparency * cov;
+                                diffuse = mk3(diffuse.x + w * il.x, diffuse.y + w * il.y, diffuse.z + w * il.z);
+                                opacity += transparency * aa;
+                        }
+                }
+                dist += step * diam;
+        }
+        return diffuse;
+}
+
 // cone_trace(root, cone, min_voxel_size) (VRT/voxel_octree.cc:276-311)
+__device__ __forceinline__ f3 cone_march_ref(const TraceParams &p, f3 o, f3 d);
+
 __device__ __forceinline__ f3 cone_march(const TraceParams &p, f3 o, f3 d)
+{
+        if (*p.lm_bad == 0u)
+                return cone_march_fast(p, o, d);
+        return cone_march_ref(p, o, d);
+}
+
+__device__ __forceinline__ f3 cone_march_ref(const TraceParams &p, f3 o, f3 d)
 {
         const float aperture = 0.577350269f, step = .1f, decay = 1.f;
         const NodeRec *__restrict__ nodes = p.r.sc.nodes;
@@ -1557,6 +1644,141 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
         }
 }
 
+// ---- split trace: primary pass, one lane per (sample, cone), film add ----
+// Primary pass: trace()'s ray_march + get_albedo + leaf compute_illum(-d);
+// slot = work unit * kRenderBlock + tid.
+__global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
+{
+        __shared__ uint32_t stk_base[kStack * kRenderBlock];
+        __shared__ uint32_t stk_ord[kStack * kRenderBlock];
+        const int tid = threadIdx.x;
+        int k, px, py, s, lx, ly;
+        if (!tile_lane(p.r, k, px, py, s, lx, ly))
+                return;
+        constexpr int kQ = 4 / VRT_RENDER_WAVES;
+        const int nb = gridDim.x, b = blockIdx.x;
+        const int u = ((nb & 7) != 0) ? b : (b & 7) * ((nb + 7) >> 3) + (b >> 3);
+        (void)kQ;
+        const int64_t slot = (int64_t)u * kRenderBlock + tid;
+        const CamParams &c = p.r.cam;
+        const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
+                                 sample_x(s), sample_y(s));
+        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
+                                 dn, c.tmin, c.tmax);
+        MarchResult m;
+        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        float4 *o = p.rec + 4 * slot;
+        if (m.hit) {
+                f3 nrm;
+                const f3 albedo = hit_albedo(p.r.sc, m, nrm);
+                const f3 direct = compute_illum(p.lm, m.node, -r.d);
+                o[0] = make_float4(m.hp.x, m.hp.y, m.hp.z, 1.f);
+                o[1] = make_float4(nrm.x, nrm.y, nrm.z, 0.f);
+                o[2] = make_float4(albedo.x, albedo.y, albedo.z, 0.f);
+                o[3] = make_float4(direct.x, direct.y, direct.z, 0.f);
+        } else {
+                const f3 sk = sky(r.d.y);
+                o[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+                o[2] = make_float4(sk.x, sk.y, sk.z, 0.f);
+        }
+}
+
+// Cones: blockIdx.y = cone i, 64 consecutive sample slots per wave (the
+// same cone of neighbouring samples: coherent node reads).  cone[i][slot] =
+// cone_trace(root, cone_i, res) (VRT/voxel_octree.cc:276-311); misses skip.
+__global__ __launch_bounds__(64) void k_cones(TraceParams p, int64_t nslots)
+{
+        const int ci = blockIdx.y;
+        const int64_t slot = (int64_t)blockIdx.x * 64 + threadIdx.x;
+        if (slot >= nslots)
+                return;
+        const float4 r0 = p.rec[4 * slot + 0];
+        if (r0.w == 0.f)
+                return;
+        const float4 r1 = p.rec[4 * slot + 1];
+        const float hx[6] = { 0.000000f, 0.000000f, 0.823639f, 0.509037f, -0.509037f, -0.823639f };
+        const float hy[6] = { 0.000000f, 0.866025f, 0.267617f, -0.700629f, -0.700629f, 0.267617f };
+        const float hz[6] = { 1.0f, 0.5f, 0.5f, 0.5f, 0.5f, 0.5f };
+        const f3 n = mk3(r1.x, r1.y, r1.z);
+        const float sg = (0.0f > n.z) ? -1.0f : 1.0f;
+        const float a0 = -1.0f / (sg + n.z);
+        const float a1 = n.x * n.y * a0;
+        const f3 t = mk3(1.0f + sg * n.x * n.x * a0, sg * a1, -sg * n.x);
+        const f3 bb = mk3(a1, sg + n.y * n.y * a0, -n.y);
+        f3 rr = mk3(0.f, 0.f, 0.f);
+        rr = rr + t * hx[ci];
+        rr = rr + bb * hy[ci];
+        rr = rr + n * hz[ci];
+        const f3 cm = cone_march(p, mk3(r0.x, r0.y, r0.z), normalize(rr));
+        float *o = p.col + 3 * ((int64_t)ci * nslots + slot);
+        o[0] = cm.x;
+        o[1] = cm.y;
+        o[2] = cm.z;
+}
+
+// Film::add(c * .25f) over the 4 samples of each pixel, in sample order,
+// into the image / tile layout of k_render; optional per-sample outputs.
+__global__ __launch_bounds__(256) void k_trace_film(TraceParams p, int64_t npix_slots)
+{
+        const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (g >= npix_slots)
+                return;
+        constexpr int kQ = 4 / VRT_RENDER_WAVES;
+        const int64_t slot0 = 4 * g;
+        const int u = (int)(slot0 / kRenderBlock);
+        const int tid0 = (int)(slot0 % kRenderBlock);
+        const int k = u / kQ;
+        const int t = p.r.rank + k * p.r.nranks;
+        const int tx = t % p.r.ntx, ty = t / p.r.ntx;
+        const int wave = (u % kQ) * VRT_RENDER_WAVES + (tid0 >> 6);
+        const int pix = (tid0 & 63) >> 2;
+        const int lx = (wave & 1) * 4 + (pix & 3), ly = (wave >> 1) * 4 + (pix >> 2);
+        const int px = tx * 8 + lx, py = ty * 8 + ly;
+        const int64_t nslots = 4 * npix_slots;
+        const float hw[6] = { 0.25f, 0.15f, 0.15f, 0.15f, 0.15f, 0.15f };
+        float acc[3] = { 0.0f, 0.0f, 0.0f };
+        for (int s = 0; s < 4; ++s) {
+                const int64_t slot = slot0 + s;
+                const float4 r0 = p.rec[4 * slot + 0], r2 = p.rec[4 * slot + 2];
+                f3 col;
+                if (r0.w != 0.f) {
+                        // diffuse += weight_i * cone_i in cone order, from zero;
+                        // get_albedo * (indirect + direct) (VRT/main.cc:22-27)
+                        f3 diffuse = mk3(0.f, 0.f, 0.f);
+                        for (int i = 0; i < 6; ++i) {
+                                const float *q = p.col + 3 * ((int64_t)i * nslots + slot);
+                                diffuse = diffuse + mk3(q[0], q[1], q[2]) * hw[i];
+                        }
+                        const float4 r3 = p.rec[4 * slot + 3];
+                        const f3 lsum = diffuse + mk3(r3.x, r3.y, r3.z);
+                        col = mk3(r2.x * lsum.x, r2.y * lsum.y, r2.z * lsum.z);
+                } else {
+                        col = mk3(r2.x, r2.y, r2.z);
+                }
+                const float c[3] = { col.x, col.y, col.z };
+                const f3 cq = col * .25f;
+                acc[0] += cq.x;
+                acc[1] += cq.y;
+                acc[2] += cq.z;
+                const size_t si = ((size_t)py * p.r.cam.nx + px) * 4 + s;
+                if (p.r.so.hit)
+                        p.r.so.hit[si] = r0.w != 0.f ? 1 : 0;
+                if (p.r.so.rgb) {
+                        p.r.so.rgb[3 * si + 0] = c[0];
+                        p.r.so.rgb[3 * si + 1] = c[1];
+                        p.r.so.rgb[3 * si + 2] = c[2];
+                }
+        }
+        float *o;
+        if (p.r.image_layout)
+                o = p.r.out + ((size_t)py * p.r.cam.nx + px) * 3;
+        else
+                o = p.r.out + ((size_t)k * 64 + ly * 8 + lx) * 3;
+        o[0] = acc[0];
+        o[1] = acc[1];
+        o[2] = acc[2];
+}
+
 __global__ void k_iota(uint32_t *v, int64_t n)
 {
         const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1613,7 +1835,24 @@ hipError_t launch_trace(const TraceParams &p, hipStream_t st)
         if (p.r.tiles_this_rank <= 0)
                 return hipSuccess;
         const int grid = (p.r.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
-        hipLaunchKernelGGL(k_trace, dim3(grid), dim3(kRenderBlock), 0, st, p);
+        if (!p.rec) {
+                hipLaunchKernelGGL(k_trace, dim3(grid), dim3(kRenderBlock), 0, st, p);
+                return hipGetLastError();
+        }
+        const int64_t nslots = (int64_t)p.r.tiles_this_rank * 256;
+        hipLaunchKernelGGL(k_trace_prim, dim3(grid), dim3(kRenderBlock), 0, st, p);
+        hipLaunchKernelGGL(k_cones, dim3((unsigned)((nslots + 63) / 64), 6), dim3(64), 0, st, p, nslots);
+        hipLaunchKernelGGL(k_trace_film, dim3((unsigned)((nslots / 4 + 255) / 256)), dim3(256), 0, st, p,
+                           nslots / 4);
+        return hipGetLastError();
+}
+
+hipError_t launch_lm_aux(const NodeRec *nodes, const LMRec *lm, int64_t n, float4 *cc, uint32_t *bad,
+                         hipStream_t st)
+{
+        if (n <= 0)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_lm_aux, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nodes, lm, n, cc, bad);
         return hipGetLastError();
 }
 
