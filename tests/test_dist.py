@@ -1,0 +1,87 @@
+"""Multi-rank frame protocol on CPU (gloo, world_size 2 and 3): the tile
+partition, packed per-rank buffers, gather to rank 0 and re-assembly of
+bench.py's primary frames, and the chunked pixel partition + SUM reduce of
+its secondary frames (voxelraytrace20190722_amd/dist.py).  Ranks render with
+the oracle (no GPU here); tests/test_gpu.py checks that the device tile
+buffers are exactly dist.pack_tiles_host of the device image."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import pyoracle as po
+import voxelraytrace20190722_amd as vrt
+from voxelraytrace20190722_amd import dist as vd
+from conftest import golden
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _scene():
+    z = golden("scene_soup.npz")
+    sd = vrt.SceneData(z["pos"], z["nrm"], z["uv"], z["mat"], z["mat_tex"], z["mat_kd"], z["tex_dims"],
+                       z["tex_off"], z["tex_data"])
+    c = z["cam0"]
+    return sd, int(z["depth"]), po.camera(float(c[0]), c[1:4], c[4:7], c[7:10])
+
+
+def _worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sd, depth, cam = _scene()
+    osc = po.Scene(sd, depth)
+    nx, ny = 44, 36  # 5 x 4 tiles + a ragged border outside the tile grid
+    img = osc.render(cam, 1.0, 1.0, nx, ny, film_index=1, nthreads=2, samples=False)
+    # primary: this rank's packed tiles -> gather -> unpack on rank 0
+    buf = torch.from_numpy(vd.pack_tiles_host(img, rank, world))
+    assert buf.numel() == vrt.tiles_per_rank(vrt.Film(1, 1, nx, ny), world) * 192
+    gl = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gl, dst=0)
+    res = {}
+    if rank == 0:
+        full = vd.unpack_tiles_host(torch.stack(gl).numpy(), nx, ny, world)
+        ref = img.copy()
+        ref[8 * (ny // 8):] = 0
+        ref[:, 8 * (nx // 8):] = 0
+        res["primary"] = bool(np.array_equal(full.view(np.uint32), ref.view(np.uint32)))
+    # secondary (config 5): own pixels of a zeroed image, SUM reduce
+    vis, _ = osc.render_secondary(cam, 1.0, 1.0, nx, ny, spp=4, nthreads=2, ids=False)
+    mine = np.where(vd.secondary_mask(nx, ny, rank, world), vis, np.float32(0))
+    t = torch.from_numpy(np.ascontiguousarray(mine))
+    dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        res["secondary"] = bool(np.array_equal(t.numpy().view(np.uint32), vis.view(np.uint32)))
+        with open(os.path.join(outdir, "res.json"), "w") as f:
+            json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_frame_protocol_gloo(tmp_path, world):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = json.load(open(tmp_path / "res.json"))
+    assert res == {"primary": True, "secondary": True}
+
+
+def test_partition_covers_every_tile_and_pixel_once():
+    for nx, ny in [(44, 36), (1920, 1080), (64, 8), (7, 7)]:
+        ntx, nty = vd.tile_grid(nx, ny)
+        for n in (1, 2, 3, 8):
+            tiles = np.concatenate([vd.rank_tiles(nx, ny, r, n) for r in range(n)])
+            assert np.array_equal(np.sort(tiles), np.arange(ntx * nty))
+            assert vd.tiles_per_rank(nx, ny, n) == vrt.tiles_per_rank(vrt.Film(1, 1, nx, ny), n)
+            m = sum(vd.secondary_mask(nx, ny, r, n).astype(int) for r in range(n))
+            area = np.zeros((ny, nx), int)
+            area[:8 * (ny // 8), :8 * (nx // 8)] = 1
+            assert np.array_equal(m, area)
