@@ -16,6 +16,7 @@ Inputs (octree, triangles, textures) are resident in HBM before timing.
 Rank 0 prints ONE JSON line on stdout; diagnostics go to stderr.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -48,6 +49,9 @@ def parse():
                    help="max_depth; default 8 = '256^3' (6 for --mode trace, as VRT/main.cc:67)")
     p.add_argument("--light-n", type=int, default=2048, help="light film side (--mode trace, VRT/main.cc:79)")
     p.add_argument("--detail", type=float, default=1.0, help="proxy tessellation (1.0 ~ 262k tris)")
+    p.add_argument("--scene", default=os.environ.get("VRT_SCENE", ""),
+                   help="OBJ file to render instead of the sponza-proxy (e.g. the real sponza.obj); "
+                        "also read from $VRT_SCENE")
     p.add_argument("--poses", type=int, default=16)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--cpu-threads", type=int, default=16)
@@ -87,10 +91,20 @@ def main():
 
     # ---- scene: built on the host, uploaded once (excluded from timing)
     t0 = time.time()
-    sd = vrt.SceneData.proxy(a.detail, 1)
+    if a.scene:
+        sd = vrt.obj2voxel(a.scene)  # tinyobj-exact ingest
+        scene_name = os.path.basename(a.scene)
+    else:
+        sd = vrt.SceneData.proxy(a.detail, 1)
+        scene_name = "sponza-proxy"
+    h = hashlib.sha256()
+    for arr in (sd.pos, sd.nrm, sd.uv, sd.mat, sd.mat_tex, sd.mat_kd, sd.tex_dims, sd.tex_data):
+        if arr is not None:
+            h.update(np.ascontiguousarray(arr).tobytes())
+    scene_hash = h.hexdigest()[:16]
     tree = vrt.VoxelOctree(sd, a.depth, device=local)
     info = tree.info
-    log(f"[rank {rank}] scene: {sd.ntri} tris, depth {a.depth}: {info.nodes} nodes, "
+    log(f"[rank {rank}] scene {scene_name} ({scene_hash}): {sd.ntri} tris, depth {a.depth}: {info.nodes} nodes, "
         f"{info.nonempty_leaves} non-empty leaves, {info.tri_refs} refs, "
         f"{info.device_bytes / 2**20:.1f} MiB on device; build {info.build_ms:.0f} ms, "
         f"upload {info.upload_ms:.0f} ms ({time.time() - t0:.1f} s total)")
@@ -330,6 +344,8 @@ def main():
                          f"8x8 tiles over {nth} threads"}
         osc.close()
 
+    data_desc = (f"OBJ scene {a.scene} (tinyobj-exact ingest)" if a.scene else
+                 "synthetic: deterministic sponza-proxy atrium (sponza.obj absent)")
     if rank == 0 and a.save_image:
         vrt.write_hdr(a.save_image, img.cpu().numpy())
     if rank == 0:
@@ -343,8 +359,9 @@ def main():
                 "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": a.steps,
                 "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
                 "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32+f64",
-                "data": "synthetic: deterministic sponza-proxy atrium (sponza.obj absent)",
-                "config": {"workload": f"full trace(): sponza-proxy ({sd.ntri} tris), max_depth {a.depth}",
+                "data": data_desc,
+                "config": {"workload": f"full trace(): {scene_name} ({sd.ntri} tris), max_depth {a.depth}",
+                           "scene_hash": scene_hash,
                            "mode": a.mode, "width": a.width, "height": a.height, "light_n": a.light_n,
                            "max_depth": a.depth, "tris": sd.ntri,
                            "parallelism": f"replicated light map, screen tiles x{world}"},
@@ -364,13 +381,13 @@ def main():
             metric = (f"Mrays/s at {a.width}x{a.height} Sponza {n_side}^3 octree "
                       f"(1 primary + {a.spp} stochastic secondary rays per hit pixel)")
             workload = (f"config 5: {a.width}x{a.height} primary hit + {a.spp} spp secondary rays, "
-                        f"sponza-proxy ({sd.ntri} tris), max_depth {a.depth}")
+                        f"{scene_name} ({sd.ntri} tris), max_depth {a.depth}")
             par = f"pixel chunks x{world}" + (f" + {coll} sum-reduce" if world > 1 else "")
         else:
             total_rays = rays_per_frame * a.steps
             mean_rays = rays_per_frame
             metric = f"Mrays/s at {a.width}x{a.height} Sponza {n_side}^3 octree (primary rays, 4 spp)"
-            workload = (f"primary render {a.width}x{a.height} x4 spp, sponza-proxy ({sd.ntri} tris), "
+            workload = (f"primary render {a.width}x{a.height} x4 spp, {scene_name} ({sd.ntri} tris), "
                         f"max_depth {a.depth} (\"{n_side}^3\")")
             par = f"screen tiles x{world}" + (f" + {coll} gather" if world > 1 else "")
         value = total_rays / elapsed / 1e6
@@ -379,8 +396,8 @@ def main():
             "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32+f64",
-            "data": "synthetic: deterministic sponza-proxy atrium (sponza.obj absent), 16-pose camera sweep",
-            "config": {"workload": workload, "mode": a.mode,
+            "data": data_desc + ", 16-pose camera sweep",
+            "config": {"workload": workload, "mode": a.mode, "scene_hash": scene_hash,
                        "width": a.width, "height": a.height, "max_depth": a.depth,
                        "rays_per_frame": int(round(mean_rays)), "tris": sd.ntri, "poses": a.poses,
                        "parallelism": par},
