@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--detail", type=float, default=1.0)
+    ap.add_argument("--mode", default="primary", choices=["primary", "secondary"])
+    ap.add_argument("--spp", type=int, default=64)
     a = ap.parse_args()
     sd = vrt.SceneData.proxy(a.detail, 1)
     film = _ffi.Film(1.0, 1.0, a.width, a.height)
@@ -62,7 +64,10 @@ def main():
         cams.append(cam)
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream(dev)
-    imgs = [torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev) for _ in libs]
+    sec = a.mode == "secondary"
+    imgs = [torch.zeros((a.height, a.width) if sec else (a.height, a.width, 3), dtype=torch.float32, device=dev)
+            for _ in libs]
+    prim = torch.zeros(a.width * a.height * 8, dtype=torch.float32, device=dev)
     times = {p: [] for p in a.libs}
     ref = None
     for r in range(a.rounds + 1):
@@ -72,8 +77,14 @@ def main():
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(st)
-                rc = L.vrt_render_tiles_device(h, C.byref(cam), C.byref(film), 0, 1, 1,
-                                               C.c_void_p(imgs[vi].data_ptr()), C.c_void_p(st.cuda_stream))
+                if sec:
+                        rc = L.vrt_render_secondary_device(h, C.byref(cam), C.byref(film), a.spp, 0, 1,
+                                                           C.c_void_p(prim.data_ptr()),
+                                                           C.c_void_p(imgs[vi].data_ptr()),
+                                                           C.c_void_p(st.cuda_stream))
+                else:
+                        rc = L.vrt_render_tiles_device(h, C.byref(cam), C.byref(film), 0, 1, 1,
+                                                       C.c_void_p(imgs[vi].data_ptr()), C.c_void_p(st.cuda_stream))
                 assert rc == 0, L.vrt_last_error()
                 e1.record(st)
                 evs.append((e0, e1))

@@ -989,15 +989,23 @@ struct SecondaryParams {
         uint32_t *s_vox;
 };
 
-__global__ __launch_bounds__(kBlock) void k_secondary(SecondaryParams p)
+#ifndef VRT_SEC_WAVES
+#define VRT_SEC_WAVES 1
+#endif
+#ifndef VRT_SEC_WAVES_PER_EU
+#define VRT_SEC_WAVES_PER_EU 6
+#endif
+constexpr int kSecBlock = 64 * VRT_SEC_WAVES;
+
+__global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(SecondaryParams p)
 {
-        __shared__ uint32_t stk_base[kStack * kBlock];
-        __shared__ uint32_t stk_ord[kStack * kBlock];
-        __shared__ float pts[4][64][3];
+        __shared__ uint32_t stk_base[kStack * kSecBlock];
+        __shared__ uint32_t stk_ord[kStack * kSecBlock];
+        __shared__ float pts[VRT_SEC_WAVES][64][3];
         const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
         const int64_t npix = (int64_t)p.W8 * p.H8;
         // this rank's k-th pixel: chunks of 64 pixels dealt round-robin
-        const int64_t k = (int64_t)blockIdx.x * 4 + wave;
+        const int64_t k = (int64_t)blockIdx.x * VRT_SEC_WAVES + wave;
         const int64_t chunk = k >> 6;
         const int64_t pix = ((chunk * p.nranks + p.rank) << 6) + (k & 63);
         if (pix >= npix)
@@ -1040,7 +1048,7 @@ __global__ __launch_bounds__(kBlock) void k_secondary(SecondaryParams p)
                 const f3 dn = normalize(nrm + pt);  // Ray{hit, n + p, res} normalises d
                 const RayK r = make_rayk(hp, dn, p.res, kFltMax);
                 MarchResult m;
-                ray_march_dispatch<false>(p.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+                ray_march_dispatch<false, kSecBlock>(p.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
                 hit = m.hit;
                 const size_t si = vi * (size_t)p.spp + lane;
                 if (p.s_hit) p.s_hit[si] = m.hit ? 1 : 0;
@@ -1079,7 +1087,8 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
         const int64_t chunks = (npix + 63) / 64;
         const int64_t mine = (chunks - rank + nranks - 1) / nranks;
         const int64_t waves = mine * 64;
-        hipLaunchKernelGGL(k_secondary, dim3((unsigned)((waves + 3) / 4)), dim3(kBlock), 0, st, sp);
+        hipLaunchKernelGGL(k_secondary, dim3((unsigned)((waves + VRT_SEC_WAVES - 1) / VRT_SEC_WAVES)),
+                           dim3(kSecBlock), 0, st, sp);
         return hipGetLastError();
 }
 
