@@ -307,6 +307,7 @@ struct vrt_scene {
         std::vector<NodeRec> nodes;
         std::vector<uint32_t> node_vox;
         std::vector<RefRec> refs;
+        std::vector<uint32_t> ref_tri;  // triangle id per leaf-list entry
         std::vector<TriPos> tri_pos;
         std::vector<TriAttr> tri_attr;
         std::vector<MatRec> mats;
@@ -536,8 +537,10 @@ static int finish_tree(vrt_scene *s, const vrt_scene_desc *d, const Box &root, c
 {
         const int64_t nnodes = (int64_t)s->nodes.size();
         s->refs.resize(refs.size());
+        s->ref_tri.resize(refs.size());
         for (size_t i = 0; i < refs.size(); ++i) {
                 const uint32_t t = (uint32_t)(refs[i] & 0xFFFFFFFFu);
+                s->ref_tri[i] = t;
                 RefRec &rr = s->refs[i];
                 std::memcpy(rr.p, d->pos + 9 * (size_t)t, sizeof rr.p);
                 rr.tri = t;
@@ -839,7 +842,7 @@ extern "C" int vrt_scene_leaves(const vrt_scene *s, uint32_t *voxel,
                 voxel[j] = lv[j].first;
                 count[j] = n;
                 for (uint32_t k = 0; k < n; ++k)
-                        tris[o++] = (int32_t)s->refs[nr.b + k].tri;
+                        tris[o++] = (int32_t)s->ref_tri[nr.b + k];
         }
         return VRT_OK;
 }

@@ -382,10 +382,36 @@ __device__ __forceinline__ bool leaf_isect_v2(const RefRec *__restrict__ refs,
 {
         bool any = false;
         float best = 0.f, best_t = 0.f;
-#pragma unroll 1
+#ifndef VRT_LEAF_UNROLL
+#define VRT_LEAF_UNROLL 1
+#endif
+#ifndef VRT_LEAF_PREFETCH
+#define VRT_LEAF_PREFETCH 0
+#endif
+#if VRT_LEAF_PREFETCH
+        // the next record's loads are issued before this one is tested
+        float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0, c2 = c0;
+        if (n) {
+                const float4 *q = reinterpret_cast<const float4 *>(refs + first);
+                c0 = q[0];
+                c1 = q[1];
+                c2 = q[2];
+        }
+#endif
+#pragma unroll VRT_LEAF_UNROLL
         for (uint32_t k = 0; k < n; ++k) {
+#if VRT_LEAF_PREFETCH
+                const float4 q0 = c0, q1 = c1, q2 = c2;
+                if (k + 1 < n) {
+                        const float4 *q = reinterpret_cast<const float4 *>(refs + first + k + 1);
+                        c0 = q[0];
+                        c1 = q[1];
+                        c2 = q[2];
+                }
+#else
                 const float4 *q = reinterpret_cast<const float4 *>(refs + first + k);
                 const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+#endif
                 const double v0x = q0.x, v0y = q0.y, v0z = q0.z;
                 const double dx = r.d.x, dy = r.d.y, dz = r.d.z;
                 // edge2, pvec = dir x edge2
@@ -434,59 +460,10 @@ __device__ __forceinline__ bool leaf_isect_v2(const RefRec *__restrict__ refs,
 }
 
 template <bool kCount>
-__device__ __forceinline__ bool leaf_isect_v1(const RefRec *__restrict__ refs,
-                                              uint32_t first, uint32_t n,
-                                              const RayK &r, MarchResult &m);
-
-template <bool kCount>
-__device__ __forceinline__ bool leaf_isect(const RefRec *__restrict__ refs,
-                                           uint32_t first, uint32_t n,
+__device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, uint32_t n,
                                            const RayK &r, MarchResult &m)
 {
-#if VRT_LEAF_V == 2
-        return leaf_isect_v2<kCount>(refs, first, n, r, m);
-#else
-        return leaf_isect_v1<kCount>(refs, first, n, r, m);
-#endif
-}
-
-// (v1: straight call of the shared mt_isect)
-template <bool kCount>
-__device__ __forceinline__ bool leaf_isect_v1(const RefRec *__restrict__ refs,
-                                           uint32_t first, uint32_t n,
-                                           const RayK &r, MarchResult &m)
-{
-        const double od[3] = { (double)r.o.x, (double)r.o.y, (double)r.o.z };
-        const double dv[3] = { (double)r.d.x, (double)r.d.y, (double)r.d.z };
-        bool any = false;
-        float best = 0.f;
-        for (uint32_t k = 0; k < n; ++k) {
-                const float4 *q = reinterpret_cast<const float4 *>(refs + first + k);
-                const float4 q0 = q[0], q1 = q[1], q2 = q[2];
-                const double p0[3] = { q0.x, q0.y, q0.z };
-                const double p1[3] = { q0.w, q1.x, q1.y };
-                const double p2[3] = { q1.z, q1.w, q2.x };
-                double t, u, v;
-                if (mt_isect(od, dv, p0, p1, p2, &t, &u, &v)) {
-                        // Triangle::isect (VRT/voxel_octree.cc:449-454)
-                        const float fu = clampf((float)u, 0, 1);
-                        const float fv = clampf((float)v, 0, 1);
-                        const f3 hp = r.o + r.d * (float)t;
-                        const float depth = length(hp - r.o);
-                        // min_element: first strict minimum
-                        if (!any || depth < best) {
-                                any = true;
-                                best = depth;
-                                m.tri = __float_as_uint(q2.y);
-                                m.u = fu;
-                                m.v = fv;
-                                m.hp = hp;
-                        }
-                }
-        }
-        if (kCount)
-                m.T += n;
-        return any;
+        return leaf_isect_v2<kCount>(sc.refs, first, n, r, m);
 }
 
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
@@ -511,7 +488,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         if (a & kLeafBit) {
                 if (kCount)
                         m.L++;
-                if (leaf_isect<kCount>(sc.refs, b, a & ~kLeafBit, r, m)) {
+                if (leaf_isect<kCount>(sc, b, a & ~kLeafBit, r, m)) {
                         m.hit = true;
                         m.node = 0;
                 }
@@ -581,7 +558,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 }
                 if (!leaf)
                         break;
-                if (leaf_isect<kCount>(sc.refs, b, nref, r, m)) {
+                if (leaf_isect<kCount>(sc, b, nref, r, m)) {
                         m.hit = true;
                         m.node = node;
                         break;
@@ -628,7 +605,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 if (kCount)
                         m.L++;
                 const uint32_t n = a & ~kLeafBit;
-                if (n && leaf_isect<kCount>(sc.refs, b, n, r, m)) {
+                if (n && leaf_isect<kCount>(sc, b, n, r, m)) {
                         m.hit = true;
                         m.node = node;
                         break;
