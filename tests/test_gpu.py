@@ -185,6 +185,34 @@ def test_full_size_frame_properties():
     assert np.array_equal(bits(so["rgb"][idx]), bits(osc.shade(rays)))
 
 
+def test_4k_depth9_frame_sample_matches_oracle():
+    """BASELINE configs[2] size (3840x2160, max_depth 9): device tile render
+    == image render, and 2000 random samples equal the oracle's."""
+    import torch
+    sd = vrt.SceneData.proxy(1.0, 1)
+    tree = vrt.VoxelOctree(sd, 9)
+    mn, mx = tree.root_box
+    fov, eye, spot, up = vrt.sweep_pose(mn, mx, 7, 16)
+    cam = vrt.Camera(fov, eye, spot, up)
+    film = vrt.Film(1, 1, 3840, 2160)
+    a, so = tree.render(cam, film, samples=True)
+    d = torch.zeros((2160, 3840, 3), dtype=torch.float32, device="cuda:0")
+    tree.render_tiles_device(cam, film, 0, 1, 1, d.data_ptr(), None)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(d.cpu().numpy()), bits(a))
+    osc = po.Scene(sd, 9)
+    oc = po.camera(fov, eye, spot, up)
+    rng = np.random.default_rng(1)
+    px = rng.integers(0, 3840, 500)
+    py = rng.integers(0, 2160, 500)
+    rays = np.concatenate([po.gen_rays4(oc, 1.0, 1.0, 3840, 2160, int(x), int(y)) for x, y in zip(px, py)])
+    o = osc.ray_march(rays)
+    idx = ((py.astype(np.int64) * 3840 + px)[:, None] * 4 + np.arange(4)).reshape(-1)
+    assert np.array_equal(so["tri"][idx], o["tri"])
+    assert np.array_equal(so["voxel"][idx], o["voxel"])
+    assert np.array_equal(bits(so["rgb"][idx]), bits(osc.shade(rays)))
+
+
 def test_edge_scenes():
     # single triangle filling the view, empty scene (all sky), depth 11
     one = vrt.SceneData(np.array([[-5, -5, -1, 5, -5, -1, 0, 5, -1]], np.float32), np.ones((1, 9), np.float32))
