@@ -282,16 +282,23 @@ def main():
         bytes_per_launch = np.mean([pose_b[k % a.poses] for k in range(a.steps)])
         achieved = bytes_per_launch / (kms.mean() * 1e-3) / 1e9
         traffic = None
+        measured = None
+        key = f"{a.width}x{a.height}_d{a.depth}_n{world}"
         try:
-            tj = json.load(open(a.traffic_json))
-            key = f"{a.width}x{a.height}_d{a.depth}_n{world}"
-            traffic = tj.get(key)
+            traffic = json.load(open(a.traffic_json)).get(key)
+        except Exception:
+            pass
+        try:
+            # the bound the kernel actually hits (rocprofv3 PMC of this
+            # workload, tools/summarize_prof.py): VALU issue, not HBM
+            measured = json.load(open(os.path.join(os.path.dirname(a.traffic_json), "pmc_derived.json"))).get(key)
         except Exception:
             pass
         nr = cnt_tot[3] and (cnt_tot / (len(poses_used) * rays_per_frame / world))
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": round(float(bytes_per_launch)),
+                "measured": measured,
                 "per_ray": {"A": round(float(nr[0]), 2), "L": round(float(nr[1]), 2),
                             "T": round(float(nr[2]), 2), "H": round(float(nr[3]), 3)}}
 

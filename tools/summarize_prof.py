@@ -82,6 +82,14 @@ def main():
         tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
         tj[a.key] = round(der["hbm_bytes_per_launch"])
         json.dump(tj, open(tj_path, "w"), indent=1, sort_keys=True)
+    # the measured bound next to the algorithmic roofline (bench.py reports it)
+    dj_path = os.path.join(dst, "pmc_derived.json")
+    dj = json.load(open(dj_path)) if os.path.exists(dj_path) else {}
+    keep = ("hbm_bytes_per_launch", "hbm_GBps", "l2_hit_rate", "valu_issue_frac", "valu_per_wave",
+            "avg_waves_per_cu", "clock_GHz")
+    dj[a.key] = {k: round(der[k], 4) for k in keep if k in der}
+    dj[a.key]["source"] = f"profiles/{a.tag}_summary.json"
+    json.dump(dj, open(dj_path, "w"), indent=1, sort_keys=True)
     print(json.dumps(out, indent=1))
 
 
