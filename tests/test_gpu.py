@@ -126,6 +126,63 @@ def test_ray_march_batch_matches_oracle(proxy_small, depth):
     assert np.array_equal(bits(g2["hit_p"]), bits(o2["hit_p"]))
 
 
+def _extreme_rays(rng, n, mn, mx):
+    """Raw rays (no normalisation) outside the kernels' fast path: huge and
+    overflowing direction components (travorder distances +-inf and NaN),
+    denormal and zero components, far origins, NaN / inf components, and
+    odd [tmin, tmax] ranges."""
+    c = (mn + mx) / 2
+    ext = (mx - mn) / 2
+    rays = np.zeros((n, 8), np.float32)
+    for i in range(n):
+        o = (c + rng.uniform(-1.2, 1.2, 3) * ext).astype(np.float32)
+        d = rng.normal(0, 1, 3).astype(np.float32)
+        k = i % 9
+        if k == 0:
+            d = (d / np.abs(d).max() * 3e38).astype(np.float32)  # distances overflow, +inf - inf = NaN
+        elif k == 1:
+            d[rng.integers(0, 3)] = np.float32(2e38) * np.sign(d[0] + 0.1)
+        elif k == 2:
+            d[rng.integers(0, 3)] = np.float32(1e-41)  # denormal component
+        elif k == 3:
+            d[:] = 0
+            d[rng.integers(0, 3)] = 1e-40
+        elif k == 4:
+            o = (o * np.float32(1e20)).astype(np.float32)  # far origin (> 2^60)
+            d = (c - o).astype(np.float32)
+        elif k == 5:
+            d[rng.integers(0, 3)] = np.nan
+        elif k == 6:
+            o[rng.integers(0, 3)] = np.inf
+        elif k == 7:
+            d = (d * np.float32(1e19)).astype(np.float32)  # |d| just above 2^64
+        rays[i, :3], rays[i, 3:6] = o, d
+        rays[i, 6], rays[i, 7] = [(0.0, vrt.FLT_MAX), (-np.inf, np.inf), (0.5, 0.1), (0.0, 0.2)][i % 4]
+    return rays
+
+
+def _same_f32(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    both_nan = np.isnan(a) & np.isnan(b)
+    return bool(np.all(both_nan | (bits(a) == bits(b))))
+
+
+@pytest.mark.parametrize("depth", [4, 7])
+def test_ray_march_extreme_rays_match_oracle(proxy_small, depth):
+    """The exact (non-fast) traversal path, including libstdc++'s insertion
+    sort on NaN distances, against the oracle's literal restatement."""
+    tree = vrt.VoxelOctree(proxy_small, depth)
+    osc = po.Scene(proxy_small, depth)
+    mn, mx = tree.root_box
+    rays = _extreme_rays(np.random.default_rng(100 + depth), 2700, mn, mx)
+    g, o = tree.ray_march(rays), osc.ray_march(rays)
+    assert o["hit"].sum() > 50
+    for key in ("hit", "tri", "voxel"):
+        assert np.array_equal(g[key], o[key]), key
+    assert _same_f32(g["hit_p"], o["hit_p"])
+    assert _same_f32(g["normal"], o["normal"])
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 def test_tile_partition_reassembles_image(proxy_small, nranks):
     """Per-rank tile renders + rank-major gather + unpack == one image render."""

@@ -647,7 +647,7 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
                 bool ok = true;
                 for (int k = 0; k < 3; ++k) {
                         const float lo = s->info.root_min[k], hi = s->info.root_max[k];
-                        ok = ok && std::fabs(lo) < 1.2676506e30f && std::fabs(hi) < 1.2676506e30f;
+                        ok = ok && std::fabs(lo) < 0x1p60f && std::fabs(hi) < 0x1p60f;  // see fast_ok()
                 }
                 s->dev.fast_ok = ok ? 1 : 0;
         }

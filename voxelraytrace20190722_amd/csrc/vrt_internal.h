@@ -71,7 +71,7 @@ struct DevScene {
         const uint8_t *tex_data;
         int32_t max_depth;
         int32_t nmat, ntex;
-        int32_t fast_ok;  // root box finite and |coords| < 2^100 (expand_v1)
+        int32_t fast_ok;  // root box finite and |coords| < 2^60 (expand_v1, fast_ok())
 };
 
 // Camera + film constants for ray generation (T1), computed on the host.

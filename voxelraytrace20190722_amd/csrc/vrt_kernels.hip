@@ -130,6 +130,54 @@ __device__ __forceinline__ uint32_t expand_v1(const float bmin[3],
                                        ((t1 >= r.tmin) & (t1 <= r.tmax)));
                 dist[i] = ((mx ? qx1 : qx0) + q[1][my]) + q[2][mz];
         }
+        if (!kFast) {
+                // exact path: libstdc++'s __insertion_sort itself (the ranks
+                // below assume a total order, which a NaN dist breaks):
+                // if (val < first) move_backward + put val first, else
+                // __unguarded_linear_insert (shift while val < prev) -- as
+                // adjacent swaps of val from position j to j-1: all of them
+                // when val < a[0], else until the first failing comparison.
+                // The permutation is one word of 3-bit fields; a child's
+                // dist is recomputed from its index with the same float ops
+                // (few live registers on this rare path).
+                auto dist_of = [&](uint32_t ci) {
+                        return (((ci & 4u) ? qx1 : qx0) + ((ci & 2u) ? q[1][1] : q[1][0])) +
+                               ((ci & 1u) ? q[2][1] : q[2][0]);
+                };
+                uint32_t perm = 0xFAC688u;  // position p holds child p
+#pragma unroll
+                for (int i = 1; i < 8; ++i) {
+                        const uint32_t vi = (perm >> (3 * i)) & 7u;
+                        const float v = dist_of(vi);
+                        const bool front = v < dist_of(perm & 7u);
+                        bool go = true;
+#pragma unroll
+                        for (int j = i; j >= 1; --j) {
+                                const uint32_t pk = (perm >> (3 * (j - 1))) & 7u;
+                                go = go && (front || v < dist_of(pk));
+                                const uint32_t sw = (perm & ~(63u << (3 * (j - 1)))) | (pk << (3 * j)) |
+                                                    (vi << (3 * (j - 1)));
+                                perm = go ? sw : perm;
+                        }
+                }
+                uint32_t hm = 0, order = 0;
+                int n = 0;
+                full_pos = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                        hm |= (uint32_t)hit[i] << i;
+#pragma unroll
+                for (int p = 0; p < 8; ++p) {
+                        const uint32_t ci = (perm >> (3 * p)) & 7u;
+                        const bool hc = (hm >> ci) & 1u;
+                        order |= hc ? (ci << (3 * n)) : 0u;
+                        n += hc ? 1 : 0;
+                        if (kFullPos)
+                                full_pos |= (uint32_t)p << (3 * ci);
+                }
+                cnt = n;
+                return order;
+        }
         // rank of each hit child among the hit children under the stable
         // (dist, index) order: j < i precedes i  <=>  !(dist_i < dist_j)
         uint32_t rk[8], fp[8];
@@ -183,6 +231,21 @@ __device__ __forceinline__ void ce4(float &da, uint32_t &ia, float &db, uint32_t
         ib = sw ? ti : ib;
 }
 
+__device__ __forceinline__ void ce4_lt(float &da, uint32_t &ia, float &db, uint32_t &ib)
+{
+        const bool sw = db < da;
+        const float td = da;
+        const uint32_t ti = ia;
+        da = sw ? db : da;
+        ia = sw ? ib : ia;
+        db = sw ? td : db;
+        ib = sw ? ti : ib;
+}
+
+// kStd: every lane's ray has tmin == +0 and tmax == FLT_MAX, so (fast path,
+// no NaN) `t >= tmin && t <= tmax` is exactly "t is +-0, +subnormal or
+// +normal" -- one v_cmp_class instead of two compares and an AND.
+template <bool kStd>
 __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float bmax[3], const RayK &r, int &cnt,
                                               uint32_t content)
 {
@@ -213,10 +276,18 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
                 const int mx = (i >> 2) & 1, my = (i >> 1) & 1, mz = i & 1;
                 const float t0 = fmaxf(fmaxf(nr[0][mx], nr[1][my]), nr[2][mz]);
                 const float t1 = fminf(fminf(fr[0][mx], fr[1][my]), fr[2][mz]);
-                const bool h = ((content >> i) & 1u) & !(t0 > t1) &
-                               (((t0 >= r.tmin) & (t0 <= r.tmax)) | ((t1 >= r.tmin) & (t1 <= r.tmax)));
+                bool in0, in1;
+                if (kStd) {
+                        in0 = __builtin_amdgcn_classf(t0, 0x1E0);  // -0, +0, +subnormal, +normal
+                        in1 = __builtin_amdgcn_classf(t1, 0x1E0);
+                } else {
+                        in0 = (t0 >= r.tmin) & (t0 <= r.tmax);
+                        in1 = (t1 >= r.tmin) & (t1 <= r.tmax);
+                }
+                const bool h = !(t0 > t1) & (in0 | in1);
                 hm |= (uint32_t)h << i;
         }
+        hm &= content;
         const int n = __popc(hm);
         cnt = n;
         if (__any(n > 4)) {
@@ -258,10 +329,15 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
                 d[k] = i < 8u ? dv : __int_as_float(0x7f800000);
                 id[k] = i;
         }
-        ce4(d[0], id[0], d[1], id[1]);
-        ce4(d[2], id[2], d[3], id[3]);
-        ce4(d[0], id[0], d[2], id[2]);
-        ce4(d[1], id[1], d[3], id[3]);
+        // The slots start in index order, so in the first two layers the
+        // element in the lower slot always has the lower index ((0,1),(2,3)
+        // trivially; (0,2),(1,3) compare a slot-{0,1} child with a
+        // slot-{2,3} one): ties keep the order and the comparison reduces
+        // to dist.  Only the last comparator (1,2) needs the index.
+        ce4_lt(d[0], id[0], d[1], id[1]);
+        ce4_lt(d[2], id[2], d[3], id[3]);
+        ce4_lt(d[0], id[0], d[2], id[2]);
+        ce4_lt(d[1], id[1], d[3], id[3]);
         ce4(d[1], id[1], d[2], id[2]);
         return (id[0] & 7u) | ((id[1] & 7u) << 3) | ((id[2] & 7u) << 6) | ((id[3] & 7u) << 9);
 }
@@ -338,7 +414,7 @@ __device__ __forceinline__ uint32_t expand_v0(const float bmin[3],
         return order;
 }
 
-template <bool kFullPos, bool kFast>
+template <bool kFullPos, bool kFast, bool kStd = false>
 __device__ __forceinline__ uint32_t expand(const float bmin[3],
                                            const float bmax[3],
                                            const RayK &r, int &cnt,
@@ -348,7 +424,7 @@ __device__ __forceinline__ uint32_t expand(const float bmin[3],
         return expand_v0<kFullPos>(bmin, bmax, r, cnt, full_pos);
 #elif VRT_EXPAND_V == 2
         if (kFast && !kFullPos)
-                return expand_v2(bmin, bmax, r, cnt, content);
+                return expand_v2<kStd>(bmin, bmax, r, cnt, content);
         return expand_v1<kFullPos, kFast>(bmin, bmax, r, cnt, full_pos, content);
 #else
         return expand_v1<kFullPos, kFast>(bmin, bmax, r, cnt, full_pos, content);
@@ -468,7 +544,7 @@ __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, u
 
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).
-template <bool kCount, bool kFast, int kS = kBlock>
+template <bool kCount, bool kFast, int kS = kBlock, bool kStd = false>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint32_t *stk_base,
                                           uint32_t *stk_ord,
@@ -496,7 +572,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         }
         int cnt;
         uint32_t fpos;
-        uint32_t order = expand<kCount, kFast>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
+        uint32_t order = expand<kCount, kFast, kStd>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
         uint32_t base = a;
         uint32_t depth = 1;  // depth of the node whose children we walk
         uint32_t nexp = 1;
@@ -542,7 +618,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                                 stk_aux[sp * kS] = fpos | (depth << 24);
                                         ++sp;
                                 }
-                                order = expand<kCount, kFast>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
+                                order = expand<kCount, kFast, kStd>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
                                 base = a;
                                 ++depth;
                                 ++nexp;
@@ -596,7 +672,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                         stk_aux[sp * kS] = fpos | (depth << 24);
                                 ++sp;
                         }
-                        order = expand<kCount, kFast>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
+                        order = expand<kCount, kFast, kStd>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
                         base = a;
                         ++depth;
                         ++nexp;
@@ -635,16 +711,18 @@ __device__ __forceinline__ RayK make_rayk(f3 o, f3 dn, float tmin, float tmax)
 }
 
 // Rays for which expand's fast path is exact (see expand_v1): finite
-// origin and direction, no non-zero denormal direction component, and
-// coordinates far from overflow (the scene's own flag covers the boxes).
+// origin and direction, no non-zero denormal direction component, |o| <
+// 2^60 and |d| < 2^64 per component (the scene's own flag bounds the boxes
+// by 2^60), so every travorder distance d.(centre - o) is finite (< 2^127):
+// never NaN, a total order.
 __device__ __forceinline__ bool fast_ok(const RayK &r)
 {
-        const float lim = 1.2676506e30f;  // 2^100
+        const float lim = 0x1p60f;
         bool ok = fabsf(r.o.x) < lim && fabsf(r.o.y) < lim && fabsf(r.o.z) < lim;
         const float d[3] = { r.d.x, r.d.y, r.d.z };
 #pragma unroll
         for (int k = 0; k < 3; ++k)
-                ok = ok && (d[k] == 0.f || (fabsf(d[k]) >= kFltMin && fabsf(d[k]) <= kFltMax));
+                ok = ok && (d[k] == 0.f || (fabsf(d[k]) >= kFltMin && fabsf(d[k]) < 0x1p64f));
         return ok;
 }
 
@@ -654,9 +732,15 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
                                                    uint32_t *sa, uint32_t *pr,
                                                    MarchResult &m)
 {
-        if (__all(sc.fast_ok && fast_ok(r)))
-                ray_march<kCount, true, kS>(sc, r, sb, so, sa, pr, m);
-        else
+#ifndef VRT_STD_RANGE
+#define VRT_STD_RANGE 1
+#endif
+        if (__all(sc.fast_ok && fast_ok(r))) {
+                if (VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
+                        ray_march<kCount, true, kS, true>(sc, r, sb, so, sa, pr, m);
+                else
+                        ray_march<kCount, true, kS>(sc, r, sb, so, sa, pr, m);
+        } else
                 ray_march<kCount, false, kS>(sc, r, sb, so, sa, pr, m);
 }
 
