@@ -274,8 +274,19 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
                 const int mx = (i >> 2) & 1, my = (i >> 1) & 1, mz = i & 1;
+#ifndef VRT_MAX3
+#define VRT_MAX3 1
+#endif
+#if VRT_MAX3
+                // one v_max3 / v_min3 per child: the compiler otherwise
+                // shares the pairwise max of two axes (24 ops instead of 16)
+                float t0, t1;
+                asm("v_max3_f32 %0, %1, %2, %3" : "=v"(t0) : "v"(nr[0][mx]), "v"(nr[1][my]), "v"(nr[2][mz]));
+                asm("v_min3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(fr[0][mx]), "v"(fr[1][my]), "v"(fr[2][mz]));
+#else
                 const float t0 = fmaxf(fmaxf(nr[0][mx], nr[1][my]), nr[2][mz]);
                 const float t1 = fminf(fminf(fr[0][mx], fr[1][my]), fr[2][mz]);
+#endif
                 bool in0, in1;
                 if (kStd) {
                         in0 = __builtin_amdgcn_classf(t0, 0x1E0);  // -0, +0, +subnormal, +normal
@@ -503,6 +514,25 @@ __device__ __forceinline__ bool leaf_isect_v2(const RefRec *__restrict__ refs,
                 const double tx = (double)r.o.x - v0x, ty = (double)r.o.y - v0y, tz = (double)r.o.z - v0z;
                 const double uu = tx * px + ty * py + tz * pz;
                 const bool pos = det > 0.000001;
+#ifndef VRT_LEAF_SIGNFOLD
+#define VRT_LEAF_SIGNFOLD 1
+#endif
+#if VRT_LEAF_SIGNFOLD
+                // det < 0 branch folded onto the det > 0 one by negation
+                // (exact; round-to-nearest is symmetric, so -(uu + vv) ==
+                // (-uu) + (-vv)): the same accept/reject decisions, without
+                // divergent sign branches
+                const double sdet = pos ? det : -det, suu = pos ? uu : -uu;
+                if (suu < 0.0 || suu > sdet)
+                        continue;
+                const double qx = ty * e1z - tz * e1y;
+                const double qy = tz * e1x - tx * e1z;
+                const double qz = tx * e1y - ty * e1x;
+                const double vv = dx * qx + dy * qy + dz * qz;
+                const double svv = pos ? vv : -vv;
+                if (svv < 0.0 || suu + svv > sdet)
+                        continue;
+#else
                 if (pos ? (uu < 0.0 || uu > det) : (uu > 0.0 || uu < det))
                         continue;
                 const double qx = ty * e1z - tz * e1y;
@@ -511,6 +541,7 @@ __device__ __forceinline__ bool leaf_isect_v2(const RefRec *__restrict__ refs,
                 const double vv = dx * qx + dy * qy + dz * qz;
                 if (pos ? (vv < 0.0 || uu + vv > det) : (vv > 0.0 || uu + vv < det))
                         continue;
+#endif
                 const double inv_det = 1.0 / det;
                 const double t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
                 // Triangle::isect (VRT/voxel_octree.cc:449-454)
@@ -546,8 +577,7 @@ __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, u
 // stack columns (stride kBlock).
 template <bool kCount, bool kFast, int kS = kBlock, bool kStd = false>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
-                                          uint32_t *stk_base,
-                                          uint32_t *stk_ord,
+                                          uint2 *stk,
                                           uint32_t *stk_aux,
                                           uint32_t *path_rem,
                                           MarchResult &m)
@@ -592,8 +622,9 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                 if (sp == 0)
                                         break;
                                 --sp;
-                                base = stk_base[sp * kS];
-                                const uint32_t w = stk_ord[sp * kS];
+                                const uint2 e = stk[sp * kS];
+                                base = e.x;
+                                const uint32_t w = e.y;
                                 order = w & 0xFFFFFFu;
                                 cnt = (int)(w >> 24);
                                 if (kCount) {
@@ -612,8 +643,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         load_node(sc.nodes, node, bmin, bmax, a, b);
                         if (!(a & kLeafBit)) {
                                 if (cnt) {
-                                        stk_base[sp * kS] = base;
-                                        stk_ord[sp * kS] = order | ((uint32_t)cnt << 24);
+                                        stk[sp * kS] = make_uint2(base, order | ((uint32_t)cnt << 24));
                                         if (kCount)
                                                 stk_aux[sp * kS] = fpos | (depth << 24);
                                         ++sp;
@@ -646,8 +676,9 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         if (sp == 0)
                                 break;
                         --sp;
-                        base = stk_base[sp * kS];
-                        const uint32_t w = stk_ord[sp * kS];
+                        const uint2 e = stk[sp * kS];
+                        base = e.x;
+                        const uint32_t w = e.y;
                         order = w & 0xFFFFFFu;
                         cnt = (int)(w >> 24);
                         if (kCount) {
@@ -666,8 +697,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 load_node(sc.nodes, node, bmin, bmax, a, b);
                 if (!(a & kLeafBit)) {
                         if (cnt) {
-                                stk_base[sp * kS] = base;
-                                stk_ord[sp * kS] = order | ((uint32_t)cnt << 24);
+                                stk[sp * kS] = make_uint2(base, order | ((uint32_t)cnt << 24));
                                 if (kCount)
                                         stk_aux[sp * kS] = fpos | (depth << 24);
                                 ++sp;
@@ -728,8 +758,7 @@ __device__ __forceinline__ bool fast_ok(const RayK &r)
 
 template <bool kCount, int kS = kBlock>
 __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const RayK &r,
-                                                   uint32_t *sb, uint32_t *so,
-                                                   uint32_t *sa, uint32_t *pr,
+                                                   uint2 *sb, uint32_t *sa, uint32_t *pr,
                                                    MarchResult &m)
 {
 #ifndef VRT_STD_RANGE
@@ -737,11 +766,11 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
 #endif
         if (__all(sc.fast_ok && fast_ok(r))) {
                 if (VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
-                        ray_march<kCount, true, kS, true>(sc, r, sb, so, sa, pr, m);
+                        ray_march<kCount, true, kS, true>(sc, r, sb, sa, pr, m);
                 else
-                        ray_march<kCount, true, kS>(sc, r, sb, so, sa, pr, m);
+                        ray_march<kCount, true, kS>(sc, r, sb, sa, pr, m);
         } else
-                ray_march<kCount, false, kS>(sc, r, sb, so, sa, pr, m);
+                ray_march<kCount, false, kS>(sc, r, sb, sa, pr, m);
 }
 
 // Triangle::get_albedo (VRT/voxel_octree.cc:472-484) with Triangle::isect's
@@ -816,8 +845,7 @@ template <bool kCount>
 __global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k_render(RenderParams p)
 {
         constexpr int kB = kRenderBlock;
-        __shared__ uint32_t stk_base[kStack * kB];
-        __shared__ uint32_t stk_ord[kStack * kB];
+        __shared__ uint2 stk[kStack * kB];
         __shared__ uint32_t stk_aux[kCount ? kStack * kB : 1];
         __shared__ uint32_t path_rem[kCount ? (kStack + 1) * kB : 1];
 
@@ -854,7 +882,7 @@ __global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k
                                  dn, c.tmin, c.tmax);
 
         MarchResult m;
-        ray_march_dispatch<kCount, kB>(p.sc, r, stk_base + tid, stk_ord + tid,
+        ray_march_dispatch<kCount, kB>(p.sc, r, stk + tid,
                                        stk_aux + (kCount ? tid : 0),
                                        path_rem + (kCount ? tid : 0), m);
 
@@ -915,8 +943,7 @@ __global__ __launch_bounds__(kBlock) void k_ray_march(DevScene sc,
                                                       int64_t n,
                                                       uint32_t *__restrict__ out)
 {
-        __shared__ uint32_t stk_base[kStack * kBlock];
-        __shared__ uint32_t stk_ord[kStack * kBlock];
+        __shared__ uint2 stk[kStack * kBlock];
         const int tid = threadIdx.x;
         const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
         if (i >= n)
@@ -925,7 +952,7 @@ __global__ __launch_bounds__(kBlock) void k_ray_march(DevScene sc,
         const RayK r = make_rayk(mk3(rr[0], rr[1], rr[2]), mk3(rr[3], rr[4], rr[5]),
                                  rr[6], rr[7]);
         MarchResult m;
-        ray_march_dispatch<false>(sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false>(sc, r, stk + tid, nullptr, nullptr, m);
         uint32_t *o = out + 9 * i;
         if (m.hit) {
                 f3 nrm;
@@ -1001,8 +1028,7 @@ __device__ __forceinline__ uint64_t pcg_advance(uint64_t s, uint64_t n)
 // over the 8*(n/8) render area, one pixel per lane -> {hit, hit xyz, normal}.
 __global__ __launch_bounds__(kBlock) void k_primary1(RenderParams p, float *__restrict__ prim)
 {
-        __shared__ uint32_t stk_base[kStack * kBlock];
-        __shared__ uint32_t stk_ord[kStack * kBlock];
+        __shared__ uint2 stk[kStack * kBlock];
         const int tid = threadIdx.x;
         const int W8 = 8 * p.ntx, H8 = 8 * p.nty;
         const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
@@ -1013,7 +1039,7 @@ __global__ __launch_bounds__(kBlock) void k_primary1(RenderParams p, float *__re
         const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py, 0.5f, 0.5f);
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]), dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false>(p.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false>(p.sc, r, stk + tid, nullptr, nullptr, m);
         float *o = prim + 8 * i;
         if (!m.hit) {
                 o[0] = 0.f;
@@ -1060,8 +1086,7 @@ constexpr int kSecBlock = 64 * VRT_SEC_WAVES;
 
 __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(SecondaryParams p)
 {
-        __shared__ uint32_t stk_base[kStack * kSecBlock];
-        __shared__ uint32_t stk_ord[kStack * kSecBlock];
+        __shared__ uint2 stk[kStack * kSecBlock];
         __shared__ float pts[VRT_SEC_WAVES][64][3];
         const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
         const int64_t npix = (int64_t)p.W8 * p.H8;
@@ -1109,7 +1134,7 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
                 const f3 dn = normalize(nrm + pt);  // Ray{hit, n + p, res} normalises d
                 const RayK r = make_rayk(hp, dn, p.res, kFltMax);
                 MarchResult m;
-                ray_march_dispatch<false, kSecBlock>(p.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+                ray_march_dispatch<false, kSecBlock>(p.sc, r, stk + tid, nullptr, nullptr, m);
                 hit = m.hit;
                 const size_t si = vi * (size_t)p.spp + lane;
                 if (p.s_hit) p.s_hit[si] = m.hit ? 1 : 0;
@@ -1332,8 +1357,7 @@ __device__ __forceinline__ bool tile_lane(const RenderParams &p, int &k, int &px
 
 __global__ __launch_bounds__(kRenderBlock) void k_light(LightParams p)
 {
-        __shared__ uint32_t stk_base[kStack * kRenderBlock];
-        __shared__ uint32_t stk_ord[kStack * kRenderBlock];
+        __shared__ uint2 stk[kStack * kRenderBlock];
         const int tid = threadIdx.x;
         int k, px, py, s, lx, ly;
         if (!tile_lane(p.r, k, px, py, s, lx, ly))
@@ -1344,7 +1368,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_light(LightParams p)
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         // canonical order: render_mt task t = tx*8 + ty (VRT/camera.h:50-56)
         const int tx = px / p.ptx, ty = py / p.pty;
         const int64_t task = (int64_t)tx * 8 + ty;
@@ -1661,8 +1685,7 @@ __device__ __forceinline__ f3 cone_trace_isect(const TraceParams &p, f3 hit, f3 
 // (VRT/main.cc:10-30, 118-123)
 __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
 {
-        __shared__ uint32_t stk_base[kStack * kRenderBlock];
-        __shared__ uint32_t stk_ord[kStack * kRenderBlock];
+        __shared__ uint2 stk[kStack * kRenderBlock];
         const int tid = threadIdx.x, lane = tid & 63;
         int k, px, py, s, lx, ly;
         if (!tile_lane(p.r, k, px, py, s, lx, ly))
@@ -1673,7 +1696,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         f3 col;
         if (m.hit) {
                 f3 nrm;
@@ -1719,8 +1742,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
 // slot = work unit * kRenderBlock + tid.
 __global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
 {
-        __shared__ uint32_t stk_base[kStack * kRenderBlock];
-        __shared__ uint32_t stk_ord[kStack * kRenderBlock];
+        __shared__ uint2 stk[kStack * kRenderBlock];
         const int tid = threadIdx.x;
         int k, px, py, s, lx, ly;
         if (!tile_lane(p.r, k, px, py, s, lx, ly))
@@ -1736,7 +1758,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk_base + tid, stk_ord + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         float4 *o = p.rec + 4 * slot;
         if (m.hit) {
                 f3 nrm;
