@@ -245,6 +245,9 @@ __device__ __forceinline__ void ce4_lt(float &da, uint32_t &ia, float &db, uint3
 // kStd: every lane's ray has tmin == +0 and tmax == FLT_MAX, so (fast path,
 // no NaN) `t >= tmin && t <= tmax` is exactly "t is +-0, +subnormal or
 // +normal" -- one v_cmp_class instead of two compares and an AND.
+#ifndef VRT_TWO_SLOT
+#define VRT_TWO_SLOT 2  // 1: two-slot path when no lane has > 2 hit children; 2: also the <= 1 shortcut
+#endif
 template <bool kStd>
 __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float bmax[3], const RayK &r, int &cnt,
                                               uint32_t content)
@@ -252,13 +255,19 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
         const float oo[3] = { r.o.x, r.o.y, r.o.z };
         const float dd[3] = { r.d.x, r.d.y, r.d.z };
         const float di[3] = { r.dinv.x, r.dinv.y, r.dinv.z };
-        float nr[3][2], fr[3][2], q[3][2];
+        float nr[3][2], fr[3][2], cm[3][2];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
                 const float h = (bmax[k] - bmin[k]) / 2.0f;
                 const float a0 = bmin[k];
                 const float b = bmin[k] + h;
                 const float c = b + h;
+                cm[k][0] = (a0 + b) * .5f;  // child centres (AABB::center)
+                cm[k][1] = (b + c) * .5f;
+                if (!kStd) {  // eager: cheaper in registers for the secondary-ray kernels
+                        cm[k][0] = dd[k] * (cm[k][0] - oo[k]);
+                        cm[k][1] = dd[k] * (cm[k][1] - oo[k]);
+                }
                 const float ta = (a0 - oo[k]) * di[k];
                 const float tb = (b - oo[k]) * di[k];
                 const float tc = (c - oo[k]) * di[k];
@@ -266,10 +275,7 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
                 fr[k][0] = fmaxf(ta, tb);
                 nr[k][1] = fminf(tb, tc);
                 fr[k][1] = fmaxf(tb, tc);
-                q[k][0] = dd[k] * ((a0 + b) * .5f - oo[k]);
-                q[k][1] = dd[k] * ((b + c) * .5f - oo[k]);
         }
-        const float qx0 = 0.0f + q[0][0], qx1 = 0.0f + q[0][1];
         uint32_t hm = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -301,6 +307,17 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
         hm &= content;
         const int n = __popc(hm);
         cnt = n;
+        if (VRT_TWO_SLOT >= 2 && __all(n <= 1))
+                return (uint32_t)__builtin_ctz(hm | 0x100u) & 7u;  // one or no hit child: nothing to order
+        // travorder distances dot(d, centre - o), finished only when some
+        // lane orders >= 2 children (camera rays, kStd)
+        float q[3][2];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+                q[k][0] = kStd ? dd[k] * (cm[k][0] - oo[k]) : cm[k][0];
+                q[k][1] = kStd ? dd[k] * (cm[k][1] - oo[k]) : cm[k][1];
+        }
+        const float qx0 = 0.0f + q[0][0], qx1 = 0.0f + q[0][1];
         if (__any(n > 4)) {
                 // rare: v1's full rank order over the same mask
                 float dist[8];
@@ -326,6 +343,21 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
                 for (int i = 0; i < 8; ++i)
                         order |= ((hm >> i) & 1u) ? ((uint32_t)i << (3 * rk[i])) : 0u;
                 return order;
+        }
+        if (VRT_TWO_SLOT && __all(n <= 2)) {
+                // common case: no lane has more than 2 hit children -- two
+                // slots, one comparator (ties keep index order: i0 < i1)
+                const uint32_t i0 = (uint32_t)__builtin_ctz(hm | 0x100u);
+                const uint32_t m1 = hm & (hm - 1u);
+                const uint32_t i1 = (uint32_t)__builtin_ctz(m1 | 0x100u);
+                auto dist_of = [&](uint32_t ci) {
+                        return (((ci & 4u) ? qx1 : qx0) + ((ci & 2u) ? q[1][1] : q[1][0])) +
+                               ((ci & 1u) ? q[2][1] : q[2][0]);
+                };
+                const float d0 = dist_of(i0);
+                const float d1 = i1 < 8u ? dist_of(i1) : __int_as_float(0x7f800000);
+                const bool sw = d1 < d0;
+                return sw ? ((i1 & 7u) | ((i0 & 7u) << 3)) : ((i0 & 7u) | ((i1 & 7u) << 3));
         }
         // up to 4 hit children into slots in index order; empty slots sort last
         float d[4];
