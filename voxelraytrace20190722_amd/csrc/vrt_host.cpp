@@ -650,6 +650,7 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
                         ok = ok && std::fabs(lo) < 0x1p60f && std::fabs(hi) < 0x1p60f;  // see fast_ok()
                 }
                 s->dev.fast_ok = ok ? 1 : 0;
+                s->dev.wide_leaves = s->refs.size() >= 8 * (size_t)std::max<int64_t>(1, s->info.nonempty_leaves);
         }
         s->info.device_bytes = (int64_t)tot;
         HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));

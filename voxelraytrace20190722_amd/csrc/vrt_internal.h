@@ -72,6 +72,7 @@ struct DevScene {
         int32_t max_depth;
         int32_t nmat, ntex;
         int32_t fast_ok;  // root box finite and |coords| < 2^60 (expand_v1, fast_ok())
+        int32_t wide_leaves;  // >= 8 records per non-empty leaf on average (leaf_isect)
 };
 
 // Camera + film constants for ray generation (T1), computed on the host.

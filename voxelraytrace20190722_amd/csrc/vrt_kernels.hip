@@ -598,16 +598,30 @@ __device__ __forceinline__ bool leaf_isect_v2(const RefRec *__restrict__ refs,
         return any;
 }
 
-template <bool kCount>
+template <bool kCount, bool kUni = true>
 __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, uint32_t n,
                                            const RayK &r, MarchResult &m)
 {
+#ifndef VRT_LEAF_UNIFORM
+#define VRT_LEAF_UNIFORM 1
+#endif
+        if (VRT_LEAF_UNIFORM && kUni && !kCount && sc.wide_leaves) {
+                // every active lane tests the same leaf (coherent rays,
+                // large leaves): the records' address and count are
+                // wave-uniform, so they come through the scalar cache.
+                // Only for scenes with large leaves (sc.wide_leaves): with
+                // a few records per leaf the check costs more than it saves
+                const uint32_t f0 = __builtin_amdgcn_readfirstlane(first);
+                const uint32_t n0 = __builtin_amdgcn_readfirstlane(n);
+                if (__all(first == f0 && n == n0))
+                        return leaf_isect_v2<kCount>(sc.refs + f0, 0, n0, r, m);
+        }
         return leaf_isect_v2<kCount>(sc.refs, first, n, r, m);
 }
 
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).
-template <bool kCount, bool kFast, int kS = kBlock, bool kStd = false>
+template <bool kCount, bool kFast, int kS = kBlock, bool kStd = false, bool kUni = true>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint2 *stk,
                                           uint32_t *stk_aux,
@@ -626,7 +640,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         if (a & kLeafBit) {
                 if (kCount)
                         m.L++;
-                if (leaf_isect<kCount>(sc, b, a & ~kLeafBit, r, m)) {
+                if (leaf_isect<kCount, kUni>(sc, b, a & ~kLeafBit, r, m)) {
                         m.hit = true;
                         m.node = 0;
                 }
@@ -696,7 +710,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 }
                 if (!leaf)
                         break;
-                if (leaf_isect<kCount>(sc, b, nref, r, m)) {
+                if (leaf_isect<kCount, kUni>(sc, b, nref, r, m)) {
                         m.hit = true;
                         m.node = node;
                         break;
@@ -743,7 +757,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 if (kCount)
                         m.L++;
                 const uint32_t n = a & ~kLeafBit;
-                if (n && leaf_isect<kCount>(sc, b, n, r, m)) {
+                if (n && leaf_isect<kCount, kUni>(sc, b, n, r, m)) {
                         m.hit = true;
                         m.node = node;
                         break;
@@ -788,7 +802,7 @@ __device__ __forceinline__ bool fast_ok(const RayK &r)
         return ok;
 }
 
-template <bool kCount, int kS = kBlock>
+template <bool kCount, int kS = kBlock, bool kUni = true>
 __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const RayK &r,
                                                    uint2 *sb, uint32_t *sa, uint32_t *pr,
                                                    MarchResult &m)
@@ -798,11 +812,11 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
 #endif
         if (__all(sc.fast_ok && fast_ok(r))) {
                 if (VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
-                        ray_march<kCount, true, kS, true>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, true, kUni>(sc, r, sb, sa, pr, m);
                 else
-                        ray_march<kCount, true, kS>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, false, kUni>(sc, r, sb, sa, pr, m);
         } else
-                ray_march<kCount, false, kS>(sc, r, sb, sa, pr, m);
+                ray_march<kCount, false, kS, false, kUni>(sc, r, sb, sa, pr, m);
 }
 
 // Triangle::get_albedo (VRT/voxel_octree.cc:472-484) with Triangle::isect's
@@ -1166,7 +1180,7 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
                 const f3 dn = normalize(nrm + pt);  // Ray{hit, n + p, res} normalises d
                 const RayK r = make_rayk(hp, dn, p.res, kFltMax);
                 MarchResult m;
-                ray_march_dispatch<false, kSecBlock>(p.sc, r, stk + tid, nullptr, nullptr, m);
+                ray_march_dispatch<false, kSecBlock, false>(p.sc, r, stk + tid, nullptr, nullptr, m);
                 hit = m.hit;
                 const size_t si = vi * (size_t)p.spp + lane;
                 if (p.s_hit) p.s_hit[si] = m.hit ? 1 : 0;
