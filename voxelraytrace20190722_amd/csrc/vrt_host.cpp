@@ -306,7 +306,9 @@ struct vrt_scene {
         int ntri = 0;
         std::vector<NodeRec> nodes;
         std::vector<uint32_t> node_vox;
-        std::vector<RefRec> refs;
+        std::vector<RefRec48> refs48;   // one of the two leaf-record formats
+        std::vector<RefRec64> refs64;   // (wide_leaves: RefRec64)
+        bool wide_leaves = false;
         std::vector<uint32_t> ref_tri;  // triangle id per leaf-list entry
         std::vector<TriPos> tri_pos;
         std::vector<TriAttr> tri_attr;
@@ -441,7 +443,6 @@ static int build_tree(vrt_scene *s, const vrt_scene_desc *d, bool on_device)
                 return fail(VRT_E_INVALID, "octree too large (%lld nodes)", (long long)nnodes);
         s->nodes.assign((size_t)nnodes, NodeRec{});
         s->node_vox.assign((size_t)nnodes, 0u);
-        s->refs.resize(refs.size());
         std::vector<Box> boxes((size_t)nnodes);
         std::vector<uint32_t> codes((size_t)nnodes);
         std::vector<int32_t> depth_of((size_t)nnodes);
@@ -536,22 +537,37 @@ static int finish_tree(vrt_scene *s, const vrt_scene_desc *d, const Box &root, c
                        int64_t ninternal)
 {
         const int64_t nnodes = (int64_t)s->nodes.size();
-        s->refs.resize(refs.size());
-        s->ref_tri.resize(refs.size());
-        for (size_t i = 0; i < refs.size(); ++i) {
-                const uint32_t t = (uint32_t)(refs[i] & 0xFFFFFFFFu);
-                s->ref_tri[i] = t;
-                RefRec &rr = s->refs[i];
-                std::memcpy(rr.p, d->pos + 9 * (size_t)t, sizeof rr.p);
-                rr.tri = t;
-                rr.pad[0] = rr.pad[1] = 0;
-        }
         int64_t leaves = 0, nonempty = 0;
         for (const NodeRec &nr : s->nodes) {
                 if (nr.a & kLeafBit) {
                         ++leaves;
                         if (nr.a & ~kLeafBit)
                                 ++nonempty;
+                }
+        }
+        s->wide_leaves = refs.size() >= 8 * (size_t)std::max<int64_t>(1, nonempty);
+        s->ref_tri.resize(refs.size());
+        if (s->wide_leaves)
+                s->refs64.resize(refs.size());
+        else
+                s->refs48.resize(refs.size());
+        for (size_t i = 0; i < refs.size(); ++i) {
+                const uint32_t t = (uint32_t)(refs[i] & 0xFFFFFFFFu);
+                s->ref_tri[i] = t;
+                const float *p = d->pos + 9 * (size_t)t;
+                if (s->wide_leaves) {
+                        RefRec64 &rr = s->refs64[i];
+                        for (int k = 0; k < 3; ++k) {
+                                rr.v0[k] = p[k];
+                                rr.e1[k] = (double)p[3 + k] - (double)p[k];  // SUB(edge1, vert1, vert0)
+                                rr.e2[k] = (double)p[6 + k] - (double)p[k];  // SUB(edge2, vert2, vert0)
+                        }
+                        rr.tri = t;
+                } else {
+                        RefRec48 &rr = s->refs48[i];
+                        std::memcpy(rr.p, p, sizeof rr.p);
+                        rr.tri = t;
+                        rr.pad[0] = rr.pad[1] = 0;
                 }
         }
         s->info.nodes = nnodes;
@@ -603,7 +619,10 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         HIPCHK(hipSetDevice(s->device));
         const size_t sz_nodes = s->nodes.size() * sizeof(NodeRec);
         const size_t sz_vox = s->node_vox.size() * sizeof(uint32_t);
-        const size_t sz_refs = std::max<size_t>(1, s->refs.size()) * sizeof(RefRec);
+        const void *refs_host = s->wide_leaves ? (const void *)s->refs64.data() : (const void *)s->refs48.data();
+        const size_t refs_bytes = s->wide_leaves ? s->refs64.size() * sizeof(RefRec64)
+                                                 : s->refs48.size() * sizeof(RefRec48);
+        const size_t sz_refs = std::max<size_t>(64, refs_bytes);
         const size_t sz_pos = std::max<size_t>(1, s->tri_pos.size()) * sizeof(TriPos);
         const size_t sz_attr = std::max<size_t>(1, s->tri_attr.size()) * sizeof(TriAttr);
         const size_t sz_mats = s->mats.size() * sizeof(MatRec);
@@ -621,8 +640,8 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         char *base = static_cast<char *>(s->d_mem);
         HIPCHK(hipMemcpy(base + off[0], s->nodes.data(), sz_nodes, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(base + off[1], s->node_vox.data(), sz_vox, hipMemcpyHostToDevice));
-        if (!s->refs.empty())
-                HIPCHK(hipMemcpy(base + off[2], s->refs.data(), s->refs.size() * sizeof(RefRec), hipMemcpyHostToDevice));
+        if (refs_bytes)
+                HIPCHK(hipMemcpy(base + off[2], refs_host, refs_bytes, hipMemcpyHostToDevice));
         if (!s->tri_pos.empty())
                 HIPCHK(hipMemcpy(base + off[3], s->tri_pos.data(), s->tri_pos.size() * sizeof(TriPos), hipMemcpyHostToDevice));
         if (!s->tri_attr.empty())
@@ -634,7 +653,7 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
                 HIPCHK(hipMemcpy(base + off[7], d->tex_data, (size_t)s->tex_bytes, hipMemcpyHostToDevice));
         s->dev.nodes = reinterpret_cast<const NodeRec *>(base + off[0]);
         s->dev.node_vox = reinterpret_cast<const uint32_t *>(base + off[1]);
-        s->dev.refs = reinterpret_cast<const RefRec *>(base + off[2]);
+        s->dev.refs = base + off[2];
         s->dev.tri_pos = reinterpret_cast<const TriPos *>(base + off[3]);
         s->dev.tri_attr = reinterpret_cast<const TriAttr *>(base + off[4]);
         s->dev.mats = reinterpret_cast<const MatRec *>(base + off[5]);
@@ -650,7 +669,7 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
                         ok = ok && std::fabs(lo) < 0x1p60f && std::fabs(hi) < 0x1p60f;  // see fast_ok()
                 }
                 s->dev.fast_ok = ok ? 1 : 0;
-                s->dev.wide_leaves = s->refs.size() >= 8 * (size_t)std::max<int64_t>(1, s->info.nonempty_leaves);
+                s->dev.wide_leaves = s->wide_leaves ? 1 : 0;
         }
         s->info.device_bytes = (int64_t)tot;
         HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));

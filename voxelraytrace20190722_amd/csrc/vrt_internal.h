@@ -26,14 +26,28 @@ struct alignas(16) NodeRec {
 static_assert(sizeof(NodeRec) == 32, "NodeRec must be 32 B");
 constexpr uint32_t kLeafBit = 0x80000000u;
 
-// One leaf-list entry with the triangle's vertices inlined (48 B, three
-// dwordx4): leaf lists are walked without a dependent index load.
-struct alignas(16) RefRec {
+// Leaf-list records, in leaf order with the vertices inlined (no dependent
+// index load in the leaf loop).  Two formats, chosen per scene:
+// RefRec48 for small leaves (fewer bytes per gather), RefRec64 for scenes
+// with >= 8 records per non-empty leaf (DevScene::wide_leaves), where the
+// leaf loop dominates and a wave often tests one leaf together.
+struct alignas(16) RefRec48 {
         float p[9];
         uint32_t tri;
         uint32_t pad[2];
 };
-static_assert(sizeof(RefRec) == 48, "RefRec must be 48 B");
+static_assert(sizeof(RefRec48) == 48, "RefRec48 must be 48 B");
+// 64 B (one cache line): vert0 as float (widened in the kernel), the
+// triangle id, and Moller-Trumbore's edge1 = vert1 - vert0, edge2 = vert2 -
+// vert0 already in double -- the same IEEE subtractions of widened floats
+// intersect_triangle3 makes (VRT/raytri.cc:209-210), done once per record.
+struct alignas(16) RefRec64 {
+        float v0[3];
+        uint32_t tri;
+        double e1[3];
+        double e2[3];
+};
+static_assert(sizeof(RefRec64) == 64, "RefRec64 must be 64 B");
 
 // Shading attributes of one triangle (64 B): normalised vertex normals
 // (Triangle::Triangle, VRT/voxel_octree.cc:426), uvs, material id.
@@ -63,7 +77,7 @@ struct alignas(16) TexRec {
 struct DevScene {
         const NodeRec *nodes;
         const uint32_t *node_vox;
-        const RefRec *refs;
+        const void *refs;  // RefRec64 if wide_leaves, else RefRec48
         const TriPos *tri_pos;
         const TriAttr *tri_attr;
         const MatRec *mats;
@@ -72,7 +86,8 @@ struct DevScene {
         int32_t max_depth;
         int32_t nmat, ntex;
         int32_t fast_ok;  // root box finite and |coords| < 2^60 (expand_v1, fast_ok())
-        int32_t wide_leaves;  // >= 8 records per non-empty leaf on average (leaf_isect)
+        int32_t wide_leaves;  // >= 8 records per non-empty leaf on average: RefRec64 records,
+                              // wave-uniform leaf loads (leaf_isect)
 };
 
 // Camera + film constants for ray generation (T1), computed on the host.

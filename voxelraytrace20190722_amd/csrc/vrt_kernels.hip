@@ -494,8 +494,8 @@ struct MarchResult {
 // differs, and inv_det = 1.0/det -- side-effect free -- is evaluated only
 // for a triangle that passes every test, so the results are identical.
 // The best hit keeps (float)t; ISect::hit = o + (float)t*d is rebuilt once.
-template <bool kCount>
-__device__ __forceinline__ bool leaf_isect_v2(const RefRec *__restrict__ refs,
+template <bool kCount, bool kR64>
+__device__ __forceinline__ bool leaf_isect_v2(const void *__restrict__ refs,
                                               uint32_t first, uint32_t n,
                                               const RayK &r, MarchResult &m)
 {
@@ -504,42 +504,38 @@ __device__ __forceinline__ bool leaf_isect_v2(const RefRec *__restrict__ refs,
 #ifndef VRT_LEAF_UNROLL
 #define VRT_LEAF_UNROLL 1
 #endif
-#ifndef VRT_LEAF_PREFETCH
-#define VRT_LEAF_PREFETCH 0
-#endif
-#if VRT_LEAF_PREFETCH
-        // the next record's loads are issued before this one is tested
-        float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0, c2 = c0;
-        if (n) {
-                const float4 *q = reinterpret_cast<const float4 *>(refs + first);
-                c0 = q[0];
-                c1 = q[1];
-                c2 = q[2];
-        }
-#endif
 #pragma unroll VRT_LEAF_UNROLL
         for (uint32_t k = 0; k < n; ++k) {
-#if VRT_LEAF_PREFETCH
-                const float4 q0 = c0, q1 = c1, q2 = c2;
-                if (k + 1 < n) {
-                        const float4 *q = reinterpret_cast<const float4 *>(refs + first + k + 1);
-                        c0 = q[0];
-                        c1 = q[1];
-                        c2 = q[2];
-                }
-#else
-                const float4 *q = reinterpret_cast<const float4 *>(refs + first + k);
-                const float4 q0 = q[0], q1 = q[1], q2 = q[2];
-#endif
+                const float4 *q = kR64 ? reinterpret_cast<const float4 *>(static_cast<const RefRec64 *>(refs) + first + k)
+                                       : reinterpret_cast<const float4 *>(static_cast<const RefRec48 *>(refs) + first + k);
+                const float4 q0 = q[0];
                 const double v0x = q0.x, v0y = q0.y, v0z = q0.z;
                 const double dx = r.d.x, dy = r.d.y, dz = r.d.z;
-                // edge2, pvec = dir x edge2
-                const double e2x = (double)q1.z - v0x, e2y = (double)q1.w - v0y, e2z = (double)q2.x - v0z;
+                // edge1 = vert1 - vert0, edge2 = vert2 - vert0 (VRT/raytri.cc:
+                // 209-210): stored in double (RefRec64) or made here in the
+                // register-frugal order edge2, pvec, edge1 (RefRec48)
+                const double2 *qd = reinterpret_cast<const double2 *>(q);
+                float4 q1, q2;
+                double2 qd1, qd2, qd3;
+                double e2x, e2y, e2z;
+                if (kR64) {
+                        qd1 = qd[1];
+                        qd2 = qd[2];
+                        qd3 = qd[3];
+                        e2x = qd2.y, e2y = qd3.x, e2z = qd3.y;
+                } else {
+                        q1 = q[1];
+                        q2 = q[2];
+                        e2x = (double)q1.z - v0x, e2y = (double)q1.w - v0y, e2z = (double)q2.x - v0z;
+                }
+                // pvec = dir x edge2
                 const double px = dy * e2z - dz * e2y;
                 const double py = dz * e2x - dx * e2z;
                 const double pz = dx * e2y - dy * e2x;
-                // edge1, det
-                const double e1x = (double)q0.w - v0x, e1y = (double)q1.x - v0y, e1z = (double)q1.y - v0z;
+                const double e1x = kR64 ? qd1.x : (double)q0.w - v0x;
+                const double e1y = kR64 ? qd1.y : (double)q1.x - v0y;
+                const double e1z = kR64 ? qd2.x : (double)q1.y - v0z;
+                // det
                 const double det = e1x * px + e1y * py + e1z * pz;
                 if (!(det > 0.000001) && !(det < -0.000001))
                         continue;  // parallel
@@ -586,7 +582,7 @@ __device__ __forceinline__ bool leaf_isect_v2(const RefRec *__restrict__ refs,
                         any = true;
                         best = depth;
                         best_t = tf;
-                        m.tri = __float_as_uint(q2.y);
+                        m.tri = __float_as_uint(kR64 ? q0.w : q2.y);
                         m.u = fu;
                         m.v = fv;
                 }
@@ -598,30 +594,31 @@ __device__ __forceinline__ bool leaf_isect_v2(const RefRec *__restrict__ refs,
         return any;
 }
 
-template <bool kCount, bool kUni = true>
+template <bool kCount, bool kUni, bool kR64>
 __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, uint32_t n,
                                            const RayK &r, MarchResult &m)
 {
 #ifndef VRT_LEAF_UNIFORM
 #define VRT_LEAF_UNIFORM 1
 #endif
-        if (VRT_LEAF_UNIFORM && kUni && !kCount && sc.wide_leaves) {
+        if (kR64 && VRT_LEAF_UNIFORM && kUni && !kCount) {
                 // every active lane tests the same leaf (coherent rays,
                 // large leaves): the records' address and count are
                 // wave-uniform, so they come through the scalar cache.
-                // Only for scenes with large leaves (sc.wide_leaves): with
+                // Only for scenes with large leaves (RefRec64 scenes): with
                 // a few records per leaf the check costs more than it saves
                 const uint32_t f0 = __builtin_amdgcn_readfirstlane(first);
                 const uint32_t n0 = __builtin_amdgcn_readfirstlane(n);
                 if (__all(first == f0 && n == n0))
-                        return leaf_isect_v2<kCount>(sc.refs + f0, 0, n0, r, m);
+                        return leaf_isect_v2<kCount, true>(static_cast<const RefRec64 *>(sc.refs) + f0, 0, n0,
+                                                           r, m);
         }
-        return leaf_isect_v2<kCount>(sc.refs, first, n, r, m);
+        return leaf_isect_v2<kCount, kR64>(sc.refs, first, n, r, m);
 }
 
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).
-template <bool kCount, bool kFast, int kS = kBlock, bool kStd = false, bool kUni = true>
+template <bool kCount, bool kFast, int kS, bool kStd, bool kUni, bool kR64>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint2 *stk,
                                           uint32_t *stk_aux,
@@ -640,7 +637,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         if (a & kLeafBit) {
                 if (kCount)
                         m.L++;
-                if (leaf_isect<kCount, kUni>(sc, b, a & ~kLeafBit, r, m)) {
+                if (leaf_isect<kCount, kUni, kR64>(sc, b, a & ~kLeafBit, r, m)) {
                         m.hit = true;
                         m.node = 0;
                 }
@@ -710,7 +707,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 }
                 if (!leaf)
                         break;
-                if (leaf_isect<kCount, kUni>(sc, b, nref, r, m)) {
+                if (leaf_isect<kCount, kUni, kR64>(sc, b, nref, r, m)) {
                         m.hit = true;
                         m.node = node;
                         break;
@@ -757,7 +754,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 if (kCount)
                         m.L++;
                 const uint32_t n = a & ~kLeafBit;
-                if (n && leaf_isect<kCount, kUni>(sc, b, n, r, m)) {
+                if (n && leaf_isect<kCount, kUni, kR64>(sc, b, n, r, m)) {
                         m.hit = true;
                         m.node = node;
                         break;
@@ -802,7 +799,7 @@ __device__ __forceinline__ bool fast_ok(const RayK &r)
         return ok;
 }
 
-template <bool kCount, int kS = kBlock, bool kUni = true>
+template <bool kCount, int kS, bool kUni, bool kR64>
 __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const RayK &r,
                                                    uint2 *sb, uint32_t *sa, uint32_t *pr,
                                                    MarchResult &m)
@@ -812,11 +809,11 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
 #endif
         if (__all(sc.fast_ok && fast_ok(r))) {
                 if (VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
-                        ray_march<kCount, true, kS, true, kUni>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, true, kUni, kR64>(sc, r, sb, sa, pr, m);
                 else
-                        ray_march<kCount, true, kS, false, kUni>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, false, kUni, kR64>(sc, r, sb, sa, pr, m);
         } else
-                ray_march<kCount, false, kS, false, kUni>(sc, r, sb, sa, pr, m);
+                ray_march<kCount, false, kS, false, kUni, kR64>(sc, r, sb, sa, pr, m);
 }
 
 // Triangle::get_albedo (VRT/voxel_octree.cc:472-484) with Triangle::isect's
@@ -882,7 +879,7 @@ __device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
 #define VRT_RENDER_WAVES 1
 #endif
 constexpr int kRenderBlock = 64 * VRT_RENDER_WAVES;
-template <bool kCount>
+template <bool kCount, bool kR64>
 #ifndef VRT_WAVES_PER_EU
 // 6 waves per SIMD (80 VGPRs, a 32-B/lane spill) measured 8% faster than
 // the unconstrained 4 waves/SIMD (99 VGPRs): the march is latency-bound.
@@ -928,7 +925,7 @@ __global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k
                                  dn, c.tmin, c.tmax);
 
         MarchResult m;
-        ray_march_dispatch<kCount, kB>(p.sc, r, stk + tid,
+        ray_march_dispatch<kCount, kB, true, kR64>(p.sc, r, stk + tid,
                                        stk_aux + (kCount ? tid : 0),
                                        path_rem + (kCount ? tid : 0), m);
 
@@ -984,6 +981,7 @@ __global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k
 // Batched gi::ray_march over arbitrary rays: one ray per lane.
 // Output record = vrt_hit {hit, tri, voxel, hit_p[3], normal[3]} (36 B).
 // ---------------------------------------------------------------------------
+template <bool kR64>
 __global__ __launch_bounds__(kBlock) void k_ray_march(DevScene sc,
                                                       const float *__restrict__ rays,
                                                       int64_t n,
@@ -998,7 +996,7 @@ __global__ __launch_bounds__(kBlock) void k_ray_march(DevScene sc,
         const RayK r = make_rayk(mk3(rr[0], rr[1], rr[2]), mk3(rr[3], rr[4], rr[5]),
                                  rr[6], rr[7]);
         MarchResult m;
-        ray_march_dispatch<false>(sc, r, stk + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kBlock, true, kR64>(sc, r, stk + tid, nullptr, nullptr, m);
         uint32_t *o = out + 9 * i;
         if (m.hit) {
                 f3 nrm;
@@ -1072,6 +1070,7 @@ __device__ __forceinline__ uint64_t pcg_advance(uint64_t s, uint64_t n)
 
 // Pass 1: pixel-centre primary ray (Camera::gen_rays1, VRT/camera.cc:77-93)
 // over the 8*(n/8) render area, one pixel per lane -> {hit, hit xyz, normal}.
+template <bool kR64>
 __global__ __launch_bounds__(kBlock) void k_primary1(RenderParams p, float *__restrict__ prim)
 {
         __shared__ uint2 stk[kStack * kBlock];
@@ -1085,7 +1084,7 @@ __global__ __launch_bounds__(kBlock) void k_primary1(RenderParams p, float *__re
         const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py, 0.5f, 0.5f);
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]), dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false>(p.sc, r, stk + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kBlock, true, kR64>(p.sc, r, stk + tid, nullptr, nullptr, m);
         float *o = prim + 8 * i;
         if (!m.hit) {
                 o[0] = 0.f;
@@ -1130,6 +1129,7 @@ struct SecondaryParams {
 #endif
 constexpr int kSecBlock = 64 * VRT_SEC_WAVES;
 
+template <bool kR64>
 __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(SecondaryParams p)
 {
         __shared__ uint2 stk[kStack * kSecBlock];
@@ -1180,7 +1180,7 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
                 const f3 dn = normalize(nrm + pt);  // Ray{hit, n + p, res} normalises d
                 const RayK r = make_rayk(hp, dn, p.res, kFltMax);
                 MarchResult m;
-                ray_march_dispatch<false, kSecBlock, false>(p.sc, r, stk + tid, nullptr, nullptr, m);
+                ray_march_dispatch<false, kSecBlock, false, kR64>(p.sc, r, stk + tid, nullptr, nullptr, m);
                 hit = m.hit;
                 const size_t si = vi * (size_t)p.spp + lane;
                 if (p.s_hit) p.s_hit[si] = m.hit ? 1 : 0;
@@ -1199,7 +1199,7 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
         const int64_t npix = (int64_t)rp.ntx * 8 * rp.nty * 8;
         if (npix <= 0)
                 return hipSuccess;
-        hipLaunchKernelGGL(k_primary1, dim3((unsigned)((npix + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+        hipLaunchKernelGGL(rp.sc.wide_leaves ? k_primary1<true> : k_primary1<false>, dim3((unsigned)((npix + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
                            rp, prim);
         SecondaryParams sp;
         sp.sc = rp.sc;
@@ -1219,7 +1219,7 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
         const int64_t chunks = (npix + 63) / 64;
         const int64_t mine = (chunks - rank + nranks - 1) / nranks;
         const int64_t waves = mine * 64;
-        hipLaunchKernelGGL(k_secondary, dim3((unsigned)((waves + VRT_SEC_WAVES - 1) / VRT_SEC_WAVES)),
+        hipLaunchKernelGGL(sp.sc.wide_leaves ? k_secondary<true> : k_secondary<false>, dim3((unsigned)((waves + VRT_SEC_WAVES - 1) / VRT_SEC_WAVES)),
                            dim3(kSecBlock), 0, st, sp);
         return hipGetLastError();
 }
@@ -1277,10 +1277,10 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 return hipSuccess;
         // round the grid up to a multiple of 8 (one slot per XCD)
         const int grid = (p.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
-        if (instrumented)
-                hipLaunchKernelGGL(k_render<true>, dim3(grid), dim3(kRenderBlock), 0, st, p);
-        else
-                hipLaunchKernelGGL(k_render<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
+        const bool w = p.sc.wide_leaves != 0;
+        void (*kern)(RenderParams) = instrumented ? (w ? k_render<true, true> : k_render<true, false>)
+                                                  : (w ? k_render<false, true> : k_render<false, false>);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kRenderBlock), 0, st, p);
         return hipGetLastError();
 }
 
@@ -1290,7 +1290,8 @@ hipError_t launch_ray_march(const DevScene &sc, const void *d_rays, int64_t n,
         if (n <= 0)
                 return hipSuccess;
         const int64_t grid = (n + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL(k_ray_march, dim3((unsigned)grid), dim3(kBlock), 0, st,
+        hipLaunchKernelGGL(sc.wide_leaves ? k_ray_march<true> : k_ray_march<false>, dim3((unsigned)grid),
+                           dim3(kBlock), 0, st,
                            sc, static_cast<const float *>(d_rays), n,
                            static_cast<uint32_t *>(d_hits));
         return hipGetLastError();
@@ -1401,6 +1402,7 @@ __device__ __forceinline__ bool tile_lane(const RenderParams &p, int &k, int &px
         return true;
 }
 
+template <bool kR64>
 __global__ __launch_bounds__(kRenderBlock) void k_light(LightParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
@@ -1414,7 +1416,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_light(LightParams p)
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         // canonical order: render_mt task t = tx*8 + ty (VRT/camera.h:50-56)
         const int tx = px / p.ptx, ty = py / p.pty;
         const int64_t task = (int64_t)tx * 8 + ty;
@@ -1729,6 +1731,7 @@ __device__ __forceinline__ f3 cone_trace_isect(const TraceParams &p, f3 hit, f3 
 
 // trace(root, ray, 5, true) per sample + Film::add(c * .25f)
 // (VRT/main.cc:10-30, 118-123)
+template <bool kR64>
 __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
@@ -1742,7 +1745,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         f3 col;
         if (m.hit) {
                 f3 nrm;
@@ -1786,6 +1789,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
 // ---- split trace: primary pass, one lane per (sample, cone), film add ----
 // Primary pass: trace()'s ray_march + get_albedo + leaf compute_illum(-d);
 // slot = work unit * kRenderBlock + tid.
+template <bool kR64>
 __global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
@@ -1804,7 +1808,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         float4 *o = p.rec + 4 * slot;
         if (m.hit) {
                 f3 nrm;
@@ -1929,7 +1933,7 @@ hipError_t launch_light(const LightParams &p, hipStream_t st)
         if (p.r.tiles_this_rank <= 0)
                 return hipSuccess;
         const int grid = (p.r.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
-        hipLaunchKernelGGL(k_light, dim3(grid), dim3(kRenderBlock), 0, st, p);
+        hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_light<true> : k_light<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
         return hipGetLastError();
 }
 
@@ -1974,11 +1978,11 @@ hipError_t launch_trace(const TraceParams &p, hipStream_t st)
                 return hipSuccess;
         const int grid = (p.r.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
         if (!p.rec) {
-                hipLaunchKernelGGL(k_trace, dim3(grid), dim3(kRenderBlock), 0, st, p);
+                hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace<true> : k_trace<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
                 return hipGetLastError();
         }
         const int64_t nslots = (int64_t)p.r.tiles_this_rank * 256;
-        hipLaunchKernelGGL(k_trace_prim, dim3(grid), dim3(kRenderBlock), 0, st, p);
+        hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace_prim<true> : k_trace_prim<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
         hipLaunchKernelGGL(k_cones, dim3((unsigned)((nslots + 63) / 64), 6), dim3(64), 0, st, p, nslots);
         hipLaunchKernelGGL(k_trace_film, dim3((unsigned)((nslots / 4 + 255) / 256)), dim3(256), 0, st, p,
                            nslots / 4);
