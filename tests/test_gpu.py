@@ -81,6 +81,26 @@ def test_render_matches_oracle_live(proxy_small, depth):
         assert np.array_equal(bits(rgb), bits(orgb))
 
 
+@pytest.mark.parametrize("depth,detail", [(3, 0.25), (6, 0.25), (6, 1.0), (8, 0.25)])
+def test_production_kernel_both_record_formats(depth, detail):
+    """The uninstrumented k_render (uniform-leaf loads, per-scene RefRec48 /
+    RefRec64 records) against the oracle: both leaf-record formats occur."""
+    sd = vrt.SceneData.proxy(detail, 2)
+    tree = vrt.VoxelOctree(sd, depth)
+    info = tree.info
+    wide = info.tri_refs >= 8 * max(1, info.nonempty_leaves)
+    assert wide == (depth <= 6), (depth, info.tri_refs, info.nonempty_leaves)
+    osc = po.Scene(sd, depth)
+    mn, mx = tree.root_box
+    for pose in (2, 9):
+        fov, eye, spot, up = vrt.sweep_pose(mn, mx, pose, 16)
+        rgb, so = tree.render(vrt.Camera(fov, eye, spot, up), vrt.Film(1, 1, 64, 64), samples=True)
+        orgb, oso = osc.render(po.camera(fov, eye, spot, up), 1.0, 1.0, 64, 64, film_index=1, nthreads=8)
+        for key in ("hit", "tri", "voxel"):
+            assert np.array_equal(so[key], oso[key]), (depth, pose, key)
+        assert np.array_equal(bits(rgb), bits(orgb)), (depth, pose)
+
+
 def _random_rays(rng, n, mn, mx):
     c = (mn + mx) / 2
     ext = (mx - mn) / 2
@@ -319,6 +339,27 @@ def test_secondary_matches_oracle_live(proxy_small, spp):
     for k in ("hit", "tri", "voxel"):
         assert np.array_equal(d[k], od[k]), k
     assert np.array_equal(bits(vis), bits(ovis))
+
+
+@pytest.mark.parametrize("depth", [3, 6, 8])
+def test_secondary_occlusion_walk_matches_ordered_walk(proxy_small, depth):
+    """Without per-ray ids the kernel runs the occlusion walk (any-hit,
+    direction-sign order): every ray's hit boolean -- hence the visibility
+    image -- must equal the ordered walk's and the oracle's."""
+    tree = vrt.VoxelOctree(proxy_small, depth)
+    osc = po.Scene(proxy_small, depth)
+    mn, mx = tree.root_box
+    for pose in (3, 11):
+        fov, eye, spot, up = vrt.sweep_pose(mn, mx, pose, 16)
+        cam = vrt.Camera(fov, eye, spot, up)
+        film = vrt.Film(1, 1, 48, 32)
+        vis_any, rays_any = tree.render_secondary(cam, film, spp=64)
+        vis, rays, d = tree.render_secondary(cam, film, spp=64, ids=True)
+        ovis, orays, _ = osc.render_secondary(po.camera(fov, eye, spot, up), 1.0, 1.0, 48, 32, spp=64)
+        assert rays_any == rays == orays
+        assert np.array_equal(bits(vis_any), bits(vis)), (depth, pose)
+        assert np.array_equal(bits(vis_any), bits(ovis)), (depth, pose)
+        assert 0 < d["hit"].sum() < d["hit"].size  # both outcomes occur
 
 
 def test_secondary_rank_partition_sums_to_image(proxy_small):

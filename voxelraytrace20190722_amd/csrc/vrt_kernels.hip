@@ -816,6 +816,195 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
                 ray_march<kCount, false, kS, false, kUni, kR64>(sc, r, sb, sa, pr, m);
 }
 
+// ---------------------------------------------------------------------------
+// Occlusion query: the boolean gi::ray_march returns, without the leaf or
+// triangle it found.  ray_march (VRT/voxel_octree.cc:131-188) returns true
+// iff some leaf whose box and every ancestor's box pass AABB3D::isect holds a
+// triangle for which intersect_triangle3 returns 1 (Triangle::isect returns
+// exactly that, VRT/voxel_octree.cc:446-448; ray_march_isect returns true iff
+// any record exists, :110-120).  travorder only decides WHICH such leaf is
+// found first, so the boolean is the same in every child order: this walk
+// visits the hit children in direction-sign order (no travorder distances,
+// no sorting) and stops at the first triangle that passes the MT tests (no
+// t, no inv_det, no nearest-record search).  The slab tests and MT tests are
+// the same IEEE operations as ray_march's.
+// ---------------------------------------------------------------------------
+
+// The 8 children's slab tests (kFast: expand_v2's planes and v_max3/v_min3;
+// otherwise expand_v1's exact select semantics) -> hit mask, bit ci.
+template <bool kFast>
+__device__ __forceinline__ uint32_t child_hit_mask(const float bmin[3], const float bmax[3], const RayK &r)
+{
+        const float oo[3] = { r.o.x, r.o.y, r.o.z };
+        const float di[3] = { r.dinv.x, r.dinv.y, r.dinv.z };
+        float nr[3][2], fr[3][2];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+                const float h = (bmax[k] - bmin[k]) / 2.0f;
+                const float a0 = kFast ? bmin[k] : bmin[k] + 0.0f * h;
+                const float b = bmin[k] + h;
+                const float a1 = kFast ? b : a0 + h;
+                const float c = b + h;
+                const float ta = (a0 - oo[k]) * di[k];
+                const float tb0 = (a1 - oo[k]) * di[k];
+                const float tb1 = kFast ? tb0 : (b - oo[k]) * di[k];
+                const float tc = (c - oo[k]) * di[k];
+                if (kFast) {
+                        nr[k][0] = fminf(ta, tb0);
+                        fr[k][0] = fmaxf(ta, tb0);
+                        nr[k][1] = fminf(tb1, tc);
+                        fr[k][1] = fmaxf(tb1, tc);
+                } else {
+                        nr[k][0] = std_min(ta, tb0);
+                        fr[k][0] = std_max(ta, tb0);
+                        nr[k][1] = std_min(tb1, tc);
+                        fr[k][1] = std_max(tb1, tc);
+                }
+        }
+        uint32_t hm = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+                const int mx = (i >> 2) & 1, my = (i >> 1) & 1, mz = i & 1;
+                float t0, t1;
+                if (kFast) {
+                        asm("v_max3_f32 %0, %1, %2, %3" : "=v"(t0) : "v"(nr[0][mx]), "v"(nr[1][my]), "v"(nr[2][mz]));
+                        asm("v_min3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(fr[0][mx]), "v"(fr[1][my]), "v"(fr[2][mz]));
+                } else {
+                        t0 = nr[0][mx];
+                        t1 = fr[0][mx];
+                        if (t0 < nr[1][my]) t0 = nr[1][my];
+                        if (t0 < nr[2][mz]) t0 = nr[2][mz];
+                        if (fr[1][my] < t1) t1 = fr[1][my];
+                        if (fr[2][mz] < t1) t1 = fr[2][mz];
+                }
+                const bool h = !(t0 > t1) & (((t0 >= r.tmin) & (t0 <= r.tmax)) | ((t1 >= r.tmin) & (t1 <= r.tmax)));
+                hm |= (uint32_t)h << i;
+        }
+        return hm;
+}
+
+// bit ci of m -> bit ci ^ s (children renumbered so that ascending order is
+// the ray's direction-sign order)
+__device__ __forceinline__ uint32_t xor_permute8(uint32_t m, uint32_t s)
+{
+        m = (s & 4u) ? (((m & 0x0Fu) << 4) | ((m >> 4) & 0x0Fu)) : m;
+        m = (s & 2u) ? (((m & 0x33u) << 2) | ((m >> 2) & 0x33u)) : m;
+        m = (s & 1u) ? (((m & 0x55u) << 1) | ((m >> 1) & 0x55u)) : m;
+        return m;
+}
+
+// true iff some record of the leaf passes intersect_triangle3's tests
+// (VRT/raytri.cc:197-249, the same operations as leaf_isect_v2)
+template <bool kR64>
+__device__ __forceinline__ bool leaf_any(const void *__restrict__ refs, uint32_t first, uint32_t n, const RayK &r)
+{
+        const double dx = r.d.x, dy = r.d.y, dz = r.d.z;
+        for (uint32_t k = 0; k < n; ++k) {
+                const float4 *q = kR64 ? reinterpret_cast<const float4 *>(static_cast<const RefRec64 *>(refs) + first + k)
+                                       : reinterpret_cast<const float4 *>(static_cast<const RefRec48 *>(refs) + first + k);
+                const float4 q0 = q[0];
+                const double v0x = q0.x, v0y = q0.y, v0z = q0.z;
+                const double2 *qd = reinterpret_cast<const double2 *>(q);
+                float4 q1, q2;
+                double2 qd1, qd2, qd3;
+                double e2x, e2y, e2z;
+                if (kR64) {
+                        qd1 = qd[1];
+                        qd2 = qd[2];
+                        qd3 = qd[3];
+                        e2x = qd2.y, e2y = qd3.x, e2z = qd3.y;
+                } else {
+                        q1 = q[1];
+                        q2 = q[2];
+                        e2x = (double)q1.z - v0x, e2y = (double)q1.w - v0y, e2z = (double)q2.x - v0z;
+                }
+                const double px = dy * e2z - dz * e2y;
+                const double py = dz * e2x - dx * e2z;
+                const double pz = dx * e2y - dy * e2x;
+                const double e1x = kR64 ? qd1.x : (double)q0.w - v0x;
+                const double e1y = kR64 ? qd1.y : (double)q1.x - v0y;
+                const double e1z = kR64 ? qd2.x : (double)q1.y - v0z;
+                const double det = e1x * px + e1y * py + e1z * pz;
+                if (!(det > 0.000001) && !(det < -0.000001))
+                        continue;
+                const double tx = (double)r.o.x - v0x, ty = (double)r.o.y - v0y, tz = (double)r.o.z - v0z;
+                const double uu = tx * px + ty * py + tz * pz;
+                const bool pos = det > 0.000001;
+                const double sdet = pos ? det : -det, suu = pos ? uu : -uu;
+                if (suu < 0.0 || suu > sdet)
+                        continue;
+                const double qx = ty * e1z - tz * e1y;
+                const double qy = tz * e1x - tx * e1z;
+                const double qz = tx * e1y - ty * e1x;
+                const double vv = dx * qx + dy * qy + dz * qz;
+                const double svv = pos ? vv : -vv;
+                if (svv < 0.0 || suu + svv > sdet)
+                        continue;
+                return true;
+        }
+        return false;
+}
+
+template <bool kFast, int kS, bool kR64>
+__device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, uint2 *stk)
+{
+        float bmin[3], bmax[3];
+        uint32_t a, b;
+        load_node(sc.nodes, 0, bmin, bmax, a, b);
+        if (!aabb_isect(bmin, bmax, r.o, r.dinv, r.tmin, r.tmax))
+                return false;
+        if (a & kLeafBit)
+                return leaf_any<kR64>(sc.refs, b, a & ~kLeafBit, r);
+        // children in ascending (ci ^ s): the near half of each axis first
+        const uint32_t s = (r.d.x < 0.f ? 4u : 0u) | (r.d.y < 0.f ? 2u : 0u) | (r.d.z < 0.f ? 1u : 0u);
+        uint32_t mask = xor_permute8(child_hit_mask<kFast>(bmin, bmax, r) & b, s);
+        uint32_t base = a;
+        int sp = 0;
+        for (;;) {
+                // advance to the next non-empty leaf (while-while, as ray_march)
+                bool leaf = false;
+                uint32_t nref = 0;
+                for (;;) {
+                        if (mask == 0) {
+                                if (sp == 0)
+                                        break;
+                                --sp;
+                                const uint2 e = stk[sp * kS];
+                                base = e.x;
+                                mask = e.y;
+                                continue;
+                        }
+                        const uint32_t ci = (uint32_t)__builtin_ctz(mask) ^ s;
+                        mask &= mask - 1u;
+                        load_node(sc.nodes, base + ci, bmin, bmax, a, b);
+                        if (!(a & kLeafBit)) {
+                                if (mask) {
+                                        stk[sp * kS] = make_uint2(base, mask);
+                                        ++sp;
+                                }
+                                mask = xor_permute8(child_hit_mask<kFast>(bmin, bmax, r) & b, s);
+                                base = a;
+                                continue;
+                        }
+                        nref = a & ~kLeafBit;  // > 0: the content mask skips empty leaves
+                        leaf = true;
+                        break;
+                }
+                if (!leaf)
+                        return false;
+                if (leaf_any<kR64>(sc.refs, b, nref, r))
+                        return true;
+        }
+}
+
+template <int kS, bool kR64>
+__device__ __forceinline__ bool ray_occluded_dispatch(const DevScene &sc, const RayK &r, uint2 *stk)
+{
+        if (__all(sc.fast_ok && fast_ok(r)))
+                return ray_occluded<true, kS, kR64>(sc, r, stk);
+        return ray_occluded<false, kS, kR64>(sc, r, stk);
+}
+
 // Triangle::get_albedo (VRT/voxel_octree.cc:472-484) with Triangle::isect's
 // normal (VRT/voxel_octree.cc:451-453).
 __device__ __forceinline__ f3 hit_albedo(const DevScene &sc, const MarchResult &m, f3 &normal)
@@ -1129,7 +1318,9 @@ struct SecondaryParams {
 #endif
 constexpr int kSecBlock = 64 * VRT_SEC_WAVES;
 
-template <bool kR64>
+// kAny (no per-ray ids requested): the visibility image needs only each
+// ray's hit boolean -> the occlusion walk (ray_occluded), same booleans.
+template <bool kR64, bool kAny>
 __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(SecondaryParams p)
 {
         __shared__ uint2 stk[kStack * kSecBlock];
@@ -1179,13 +1370,18 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
                 const f3 pt = mk3(pts[wave][lane][0], pts[wave][lane][1], pts[wave][lane][2]);
                 const f3 dn = normalize(nrm + pt);  // Ray{hit, n + p, res} normalises d
                 const RayK r = make_rayk(hp, dn, p.res, kFltMax);
-                MarchResult m;
-                ray_march_dispatch<false, kSecBlock, false, kR64>(p.sc, r, stk + tid, nullptr, nullptr, m);
-                hit = m.hit;
                 const size_t si = vi * (size_t)p.spp + lane;
-                if (p.s_hit) p.s_hit[si] = m.hit ? 1 : 0;
-                if (p.s_tri) p.s_tri[si] = m.hit ? (int32_t)m.tri : -1;
-                if (p.s_vox) p.s_vox[si] = m.hit ? p.sc.node_vox[m.node] : 0xFFFFFFFFu;
+                if (kAny) {
+                        hit = ray_occluded_dispatch<kSecBlock, kR64>(p.sc, r, stk + tid);
+                        if (p.s_hit) p.s_hit[si] = hit ? 1 : 0;
+                } else {
+                        MarchResult m;
+                        ray_march_dispatch<false, kSecBlock, false, kR64>(p.sc, r, stk + tid, nullptr, nullptr, m);
+                        hit = m.hit;
+                        if (p.s_hit) p.s_hit[si] = m.hit ? 1 : 0;
+                        if (p.s_tri) p.s_tri[si] = m.hit ? (int32_t)m.tri : -1;
+                        if (p.s_vox) p.s_vox[si] = m.hit ? p.sc.node_vox[m.node] : 0xFFFFFFFFu;
+                }
         }
         const uint64_t hm = __ballot(hit);
         if (lane == 0)
@@ -1219,8 +1415,14 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
         const int64_t chunks = (npix + 63) / 64;
         const int64_t mine = (chunks - rank + nranks - 1) / nranks;
         const int64_t waves = mine * 64;
-        hipLaunchKernelGGL(sp.sc.wide_leaves ? k_secondary<true> : k_secondary<false>, dim3((unsigned)((waves + VRT_SEC_WAVES - 1) / VRT_SEC_WAVES)),
-                           dim3(kSecBlock), 0, st, sp);
+#ifndef VRT_SEC_ANY
+#define VRT_SEC_ANY 1
+#endif
+        const bool any = VRT_SEC_ANY && !s_tri && !s_vox;
+        void (*kern)(SecondaryParams) = sp.sc.wide_leaves ? (any ? k_secondary<true, true> : k_secondary<true, false>)
+                                                          : (any ? k_secondary<false, true> : k_secondary<false, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)((waves + VRT_SEC_WAVES - 1) / VRT_SEC_WAVES)), dim3(kSecBlock), 0,
+                           st, sp);
         return hipGetLastError();
 }
 
