@@ -992,6 +992,21 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
                 }
                 if (!leaf)
                         return false;
+#ifndef VRT_SEC_UNI
+#define VRT_SEC_UNI 1
+#endif
+                if (kR64 && VRT_SEC_UNI) {
+                        // large leaves: when every active lane tests the same
+                        // leaf (rays of one origin), the records come through
+                        // the scalar cache (as leaf_isect)
+                        const uint32_t f0 = __builtin_amdgcn_readfirstlane(b);
+                        const uint32_t n0 = __builtin_amdgcn_readfirstlane(nref);
+                        if (__all(b == f0 && nref == n0)) {
+                                if (leaf_any<true>(static_cast<const RefRec64 *>(sc.refs) + f0, 0, n0, r))
+                                        return true;
+                                continue;
+                        }
+                }
                 if (leaf_any<kR64>(sc.refs, b, nref, r))
                         return true;
         }
