@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--kernel", default="k_render<false>")
+    ap.add_argument("--kernel", default="k_render<false, false>")
     ap.add_argument("--key", default="1920x1080_d8_n1")
     ap.add_argument("--src", default=None)
     a = ap.parse_args()
