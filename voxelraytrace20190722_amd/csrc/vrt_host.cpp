@@ -628,16 +628,17 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         const size_t sz_mats = s->mats.size() * sizeof(MatRec);
         const size_t sz_texs = std::max<size_t>(1, s->texs.size()) * sizeof(TexRec);
         const size_t sz_tex = (size_t)std::max<int64_t>(16, s->tex_bytes);
-        size_t off[9];
+        size_t off[10];
         size_t tot = 0;
-        const size_t sizes[8] = { sz_nodes, sz_vox, sz_refs, sz_pos, sz_attr, sz_mats, sz_texs, sz_tex };
-        for (int i = 0; i < 8; ++i) {
+        const size_t sizes[9] = { sz_nodes, sz_vox, sz_refs, sz_pos, sz_attr, sz_mats, sz_texs, sz_tex, kCtrBytes };
+        for (int i = 0; i < 9; ++i) {
                 off[i] = tot;
                 tot += align_up(sizes[i]);
         }
-        off[8] = tot;
+        off[9] = tot;
         HIPCHK(hipMalloc(&s->d_mem, tot));
         char *base = static_cast<char *>(s->d_mem);
+        HIPCHK(hipMemset(base + off[8], 0, kCtrBytes));
         HIPCHK(hipMemcpy(base + off[0], s->nodes.data(), sz_nodes, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(base + off[1], s->node_vox.data(), sz_vox, hipMemcpyHostToDevice));
         if (refs_bytes)
@@ -659,6 +660,7 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         s->dev.mats = reinterpret_cast<const MatRec *>(base + off[5]);
         s->dev.texs = reinterpret_cast<const TexRec *>(base + off[6]);
         s->dev.tex_data = reinterpret_cast<const uint8_t *>(base + off[7]);
+        s->dev.ctr = reinterpret_cast<uint32_t *>(base + off[8]);
         s->dev.max_depth = s->max_depth;
         s->dev.nmat = (int32_t)s->mats.size();
         s->dev.ntex = (int32_t)s->texs.size();

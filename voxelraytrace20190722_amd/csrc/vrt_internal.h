@@ -88,7 +88,11 @@ struct DevScene {
         int32_t fast_ok;  // root box finite and |coords| < 2^60 (expand_v1, fast_ok())
         int32_t wide_leaves;  // >= 8 records per non-empty leaf on average: RefRec64 records,
                               // wave-uniform leaf loads (leaf_isect)
+        uint32_t *ctr;        // k_render_p work counters: [x * kCtrStride], x = 0..7 per XCD,
+                              // 8 = finished waves; zero between launches
 };
+constexpr int kCtrStride = 32;  // one 128-B line per counter
+constexpr size_t kCtrBytes = 9 * kCtrStride * sizeof(uint32_t);
 
 // Camera + film constants for ray generation (T1), computed on the host.
 struct CamParams {

@@ -1083,39 +1083,15 @@ __device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
 #define VRT_RENDER_WAVES 1
 #endif
 constexpr int kRenderBlock = 64 * VRT_RENDER_WAVES;
-template <bool kCount, bool kR64>
-#ifndef VRT_WAVES_PER_EU
-// 6 waves per SIMD (80 VGPRs, a 32-B/lane spill) measured 8% faster than
-// the unconstrained 4 waves/SIMD (99 VGPRs): the march is latency-bound.
-#define VRT_WAVES_PER_EU 6
-#endif
-__global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k_render(RenderParams p)
+// One work unit of the primary render: the 4x4-pixel quadrant `wave` of
+// this rank's k-th 8x8 tile, 4 gen_rays4 samples per pixel, one ray per
+// lane (lane = 4*pixel + sample).  stk_* are this lane's LDS stack columns.
+template <bool kCount, bool kR64, int kS>
+__device__ __forceinline__ void render_unit(const RenderParams &p, int k, int wave, int lane, uint2 *stk,
+                                            uint32_t *stk_aux, uint32_t *path_rem)
 {
-        constexpr int kB = kRenderBlock;
-        __shared__ uint2 stk[kStack * kB];
-        __shared__ uint32_t stk_aux[kCount ? kStack * kB : 1];
-        __shared__ uint32_t path_rem[kCount ? (kStack + 1) * kB : 1];
-
-        const int tid = threadIdx.x;
-        // XCD-aware order: blocks b, b+8, ... run on one XCD; give them
-        // consecutive work units (a unit = kUnitsPerTile-th of an 8x8 tile)
-        // so each XCD's L2 serves one screen region.
-        constexpr int kQ = 4 / VRT_RENDER_WAVES;  // units per tile
-        const int nb = gridDim.x;
-        const int b = blockIdx.x;
-        const int per = (nb + 7) >> 3;
-        const int xcd = b & 7, slot = b >> 3;
-        int u = xcd * per + slot;
-        if ((nb & 7) != 0) {
-                // uneven grid: fall back to the identity map
-                u = b;
-        }
-        if (u >= p.tiles_this_rank * kQ)
-                return;
-        const int k = u / kQ;
         const int t = p.rank + k * p.nranks;
         const int tx = t % p.ntx, ty = t / p.ntx;
-        const int wave = (u % kQ) * VRT_RENDER_WAVES + (tid >> 6), lane = tid & 63;
         const int s = lane & 3, pix = lane >> 2;
         const int lx = (wave & 1) * 4 + (pix & 3);
         const int ly = (wave >> 1) * 4 + (pix >> 2);
@@ -1129,9 +1105,7 @@ __global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k
                                  dn, c.tmin, c.tmax);
 
         MarchResult m;
-        ray_march_dispatch<kCount, kB, true, kR64>(p.sc, r, stk + tid,
-                                       stk_aux + (kCount ? tid : 0),
-                                       path_rem + (kCount ? tid : 0), m);
+        ray_march_dispatch<kCount, kS, true, kR64>(p.sc, r, stk, stk_aux, path_rem, m);
 
         f3 col;
         if (m.hit) {
@@ -1178,6 +1152,89 @@ __global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k
                 o[0] = acc[0];
                 o[1] = acc[1];
                 o[2] = acc[2];
+        }
+}
+
+template <bool kCount, bool kR64>
+#ifndef VRT_WAVES_PER_EU
+// 6 waves per SIMD (80 VGPRs, a 32-B/lane spill) measured 8% faster than
+// the unconstrained 4 waves/SIMD (99 VGPRs): the march is latency-bound.
+#define VRT_WAVES_PER_EU 6
+#endif
+__global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k_render(RenderParams p)
+{
+        constexpr int kB = kRenderBlock;
+        __shared__ uint2 stk[kStack * kB];
+        __shared__ uint32_t stk_aux[kCount ? kStack * kB : 1];
+        __shared__ uint32_t path_rem[kCount ? (kStack + 1) * kB : 1];
+
+        const int tid = threadIdx.x;
+        // XCD-aware order: blocks b, b+8, ... run on one XCD; give them
+        // consecutive work units (a unit = kUnitsPerTile-th of an 8x8 tile)
+        // so each XCD's L2 serves one screen region.
+        constexpr int kQ = 4 / VRT_RENDER_WAVES;  // units per tile
+        const int nb = gridDim.x;
+        const int b = blockIdx.x;
+        const int per = (nb + 7) >> 3;
+        const int xcd = b & 7, slot = b >> 3;
+        int u = xcd * per + slot;
+        if ((nb & 7) != 0) {
+                // uneven grid: fall back to the identity map
+                u = b;
+        }
+        if (u >= p.tiles_this_rank * kQ)
+                return;
+        const int k = u / kQ;
+        const int wave = (u % kQ) * VRT_RENDER_WAVES + (tid >> 6), lane = tid & 63;
+        render_unit<kCount, kR64, kB>(p, k, wave, lane, stk + tid, stk_aux + (kCount ? tid : 0),
+                                      path_rem + (kCount ? tid : 0));
+}
+
+// Persistent variant (uninstrumented): 4-wave workgroups sized to fill the
+// chip once; every wave pulls quadrant units from a per-XCD counter (blocks
+// b, b+8, ... share an XCD and its L2; an XCD's counter covers one
+// contiguous slice of the tiles) and moves on to the other XCDs' counters
+// when its own is exhausted.  One-wave workgroups top out at 16 resident
+// waves per CU (the per-CU workgroup limit); here 24 are resident and a
+// wave never waits for a workgroup sibling.  The last wave out resets the
+// counters for the next launch (stream order; a scene renders on one
+// stream at a time).
+constexpr int kPersistBlock = 256;
+#ifndef VRT_PERSIST_WAVES_PER_EU
+#define VRT_PERSIST_WAVES_PER_EU 5
+#endif
+template <bool kR64>
+__global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_render_p(RenderParams p)
+{
+        __shared__ uint2 stk[kStack * kPersistBlock];
+        const int tid = threadIdx.x, lane = tid & 63;
+        uint32_t *ctr = p.sc.ctr;
+        const int units = p.tiles_this_rank * 4;
+        const int per = (units + 7) >> 3;
+        const int xcd = blockIdx.x & 7;
+        for (int j = 0; j < 8; ++j) {
+                const int x = (xcd + j) & 7;
+                const int lo = x * per, hi = min(units, lo + per);
+                if (lo >= hi)
+                        continue;
+                for (;;) {
+                        uint32_t u = 0;
+                        if (lane == 0)
+                                u = atomicAdd(ctr + x * kCtrStride, 1u);
+                        u = __builtin_amdgcn_readfirstlane(u);
+                        const int unit = lo + (int)u;
+                        if (unit >= hi)
+                                break;
+                        render_unit<false, kR64, kPersistBlock>(p, unit >> 2, unit & 3, lane, stk + tid, nullptr,
+                                                                nullptr);
+                }
+        }
+        if (lane == 0) {
+                const uint32_t nw = gridDim.x * (kPersistBlock / 64);
+                if (atomicAdd(ctr + 8 * kCtrStride, 1u) == nw - 1u) {
+                        for (int x = 0; x <= 8; ++x)
+                                atomicExch(ctr + x * kCtrStride, 0u);
+                }
         }
 }
 
@@ -1495,6 +1552,35 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
         // round the grid up to a multiple of 8 (one slot per XCD)
         const int grid = (p.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
         const bool w = p.sc.wide_leaves != 0;
+#ifndef VRT_PERSIST
+#define VRT_PERSIST 1
+#endif
+        // persistent waves for RefRec48 scenes; large-leaf (RefRec64) scenes
+        // keep one-wave workgroups (-11 % persistent at depth 6)
+        if (VRT_PERSIST && !instrumented && !w && p.sc.ctr) {
+                // one resident generation of 4-wave workgroups (<= one per
+                // 4 units, a multiple of 8 for the XCD map)
+                static int blocks[2] = { 0, 0 };
+                int &nb = blocks[w ? 1 : 0];
+                if (nb == 0) {
+                        void (*kp)(RenderParams) = w ? k_render_p<true> : k_render_p<false>;
+                        int per_cu = 0, dev = 0;
+                        hipDeviceProp_t prop;
+                        hipError_t e = hipGetDevice(&dev);
+                        if (e == hipSuccess)
+                                e = hipGetDeviceProperties(&prop, dev);
+                        if (e == hipSuccess)
+                                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kPersistBlock, 0);
+                        if (e != hipSuccess)
+                                return e;
+                        nb = std::max(8, (per_cu * prop.multiProcessorCount) & ~7);
+                }
+                const int need = (p.tiles_this_rank + 7) & ~7;  // 4 units per tile, 4 waves per block
+                const int g = std::min(nb, need);
+                hipLaunchKernelGGL(w ? k_render_p<true> : k_render_p<false>, dim3(g), dim3(kPersistBlock), 0, st,
+                                   p);
+                return hipGetLastError();
+        }
         void (*kern)(RenderParams) = instrumented ? (w ? k_render<true, true> : k_render<true, false>)
                                                   : (w ? k_render<false, true> : k_render<false, false>);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kRenderBlock), 0, st, p);
