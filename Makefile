@@ -17,7 +17,7 @@ HIPFLAGS := -x hip --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 $(FP) -Iinclude -
 CXXFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Wall -fvisibility=hidden
 
 HOSTOBJS := $(BLD)/vrt_host.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o
-OBJS := $(BLD)/vrt_kernels.o $(BLD)/vrt_sort.o $(BLD)/vrt_build.o $(HOSTOBJS)
+OBJS := $(BLD)/vrt_kernels.o $(BLD)/vrt_sort.o $(BLD)/vrt_build.o $(HOSTOBJS) $(BLD)/vrt_build_id.o
 HDRS := include/vrt.h $(SRC)/vrt_math.h $(SRC)/vrt_internal.h $(SRC)/vrt_error.h
 
 all: $(PKG)/libvrt.so oracle
@@ -48,6 +48,16 @@ $(BLD)/vrt_obj.o: $(SRC)/vrt_obj.cpp include/vrt.h $(SRC)/vrt_error.h | $(BLD)
 
 $(BLD)/vrt_tga.o: $(SRC)/vrt_tga.cpp include/vrt.h $(SRC)/vrt_error.h | $(BLD)
 	g++ $(CXXFLAGS) -c $< -o $@
+
+# vrt_build_id(): the source hash (tools/build_id.py); the C file is
+# rewritten only when the hash changes
+$(BLD)/vrt_build_id.c: FORCE | $(BLD)
+	python3 tools/build_id.py --write $@
+
+$(BLD)/vrt_build_id.o: $(BLD)/vrt_build_id.c
+	gcc -O2 -fPIC -c $< -o $@
+
+FORCE:
 
 $(PKG)/libvrt.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread
@@ -80,4 +90,4 @@ clean:
 	rm -rf build $(PKG)/libvrt.so
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle isa clean
+.PHONY: all oracle isa clean FORCE

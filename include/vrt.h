@@ -218,6 +218,22 @@ int vrt_ray_march_batch_device(vrt_scene *s, const vrt_ray *d_rays, int64_t n,
 int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
                         const float *sat_in, int32_t *sat_out, int64_t n);
 
+/* The kernels' own travorder sort (std::sort of the 8 Items by dist,
+ * VRT/voxel_octree.cc:77-97) and ray_march_isect min_element
+ * (VRT/voxel_octree.cc:122-125) on arbitrary inputs, for the pin against
+ * the real libstdc++ (tests/golden/travorder_std.cpp).  Per case i:
+ * dist[8i..8i+7] and hit_mask[i] (bit ci = child ci's slab test passed) ->
+ * orders[6i..6i+5] = {full insertion-sort order (3-bit fields), exact-path
+ * hit order | count << 24, rank order | count << 24, two-slot order,
+ * 4-slot network order, full-position word} (the last four are the
+ * NaN-free fast paths).  Per record list j: depth[j*stride .. +len[j]) ->
+ * argmin[j] (the first minimum, -1 when empty). */
+int vrt_device_selftest_order(int device, const float *dist,
+                              const uint32_t *hit_mask, int64_t n,
+                              uint32_t *orders, const float *depth,
+                              const int32_t *len, int64_t m, int32_t stride,
+                              int32_t *argmin);
+
 /* ---- full trace() (VRT/main.cc:10-30, 79-123) -------
  * The reference's actual image: a light pass from a light camera
  * (render_mt + gen_rays4; every hit adds clamp(dot(illum_d[i], n), 0, 1) *
@@ -283,6 +299,16 @@ int intersect_triangle3(double orig[3], double dir[3], double vert0[3],
 /* VRT/tribox2.h:6 */
 int triBoxOverlap(float boxcenter[3], float boxhalfsize[3],
                   float triverts[3][3]);
+/* VRT/stb_image_write.h:178 (stb_image_write v1.13, called at VRT/main.cc:126):
+ * the same function as vrt_write_hdr, under the reference's name, so a
+ * caller of the reference's writer relinks without renaming the call. */
+int stbi_write_hdr(char const *filename, int w, int h, int comp,
+                   const float *data);
+
+/* ---- build identity ---------------------------------------------------- */
+/* Source hash this library was built from (tools/build_id.py: sha256 of
+ * csrc/, include/vrt.h and the Makefile, 16 hex digits). */
+const char *vrt_build_id(void);
 
 /* ---- scene ingest (VRT/voxel_octree.cc:305-388) -------------------------
  * vrt_obj_load = obj2voxel(path) + load_image for every texture a face

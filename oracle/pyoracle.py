@@ -44,6 +44,8 @@ def oracle():
             "ora_gen_rays1": (C.c_int, [f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, f32p]),
             "ora_make_ray": (None, [f32p, f32p, C.c_float, C.c_float, f32p]),
             "ora_aabb_isect": (C.c_int, [f32p, f32p]),
+            "ora_sort8": (None, [f32p, i32p]),
+            "ora_first_min": (C.c_int, [f32p, C.c_int]),
             "ora_scene_create": (P, [f32p, f32p, f32p, i32p, C.c_int, C.c_int]),
             "ora_scene_set_materials": (None, [P, C.c_int, i32p, f32p, C.c_int, i32p, i64p, u8p, C.c_int64]),
             "ora_scene_destroy": (None, [P]),
@@ -75,6 +77,20 @@ def oracle():
             f.argtypes = args
         _o = L
     return _o
+
+
+def sort8(dist):
+    """travorder's std::sort of the 8 Items by dist -> child order (8,)."""
+    d = np.ascontiguousarray(np.asarray(dist, np.float32).reshape(8))
+    o = np.zeros(8, np.int32)
+    oracle().ora_sort8(_p(d, f32p), _p(o, i32p))
+    return o
+
+
+def first_min(depth):
+    """ray_march_isect's std::min_element index (-1 if empty)."""
+    d = np.ascontiguousarray(np.asarray(depth, np.float32).reshape(-1))
+    return int(oracle().ora_first_min(_p(d, f32p), d.shape[0]))
 
 
 def reference_available():

@@ -667,18 +667,18 @@ static int march_isect(const ora_scene *s, const onode *leaf, const float r[8],
         return 1;
 }
 
-/* travorder: 8 dot products + std::sort (insertion sort for 8 elements in
- * libstdc++: __insertion_sort / __unguarded_linear_insert, strict <) */
-static void travorder(const ora_scene *s, const onode *nd, const float r[8],
-                      int ord[8])
+/* std::sort(items, items + 8, lhs.dist < rhs.dist) (VRT/voxel_octree.cc:
+ * 91-93): for 8 elements libstdc++ runs __insertion_sort alone
+ * (stl_algo.h:1855 threshold 16, :1826 move-to-front when val < first, :1806
+ * __unguarded_linear_insert shifting while val < prev) -- restated on the
+ * child indices.  Pinned against the real libstdc++ by
+ * tests/golden/travorder_std.npz. */
+void ora_sort8(const float dist[8], int ord[8])
 {
         struct { int ci; float dist; } it[8], val;
-        v3 o = vget(r), d = vget(r + 3);
         for (int ci = 0; ci < 8; ++ci) {
-                const float *b = s->nodes[nd->child + ci].box;
-                v3 c = muls(add(vget(b), vget(b + 3)), .5f); /* center() */
                 it[ci].ci = ci;
-                it[ci].dist = dot(d, sub(c, o));
+                it[ci].dist = dist[ci];
         }
         for (int i = 1; i < 8; ++i) {
                 val = it[i];
@@ -696,6 +696,33 @@ static void travorder(const ora_scene *s, const onode *nd, const float r[8],
         }
         for (int i = 0; i < 8; ++i)
                 ord[i] = it[i].ci;
+}
+
+/* std::min_element(records, lhs.depth < rhs.depth) (VRT/voxel_octree.cc:
+ * 122-125): the first element, replaced only by a strictly smaller one;
+ * -1 for an empty range.  Pinned like ora_sort8. */
+int ora_first_min(const float *depth, int n)
+{
+        int best = n > 0 ? 0 : -1;
+        for (int i = 1; i < n; ++i)
+                if (depth[i] < depth[best])
+                        best = i;
+        return best;
+}
+
+/* travorder (VRT/voxel_octree.cc:77-97): dot(ray.d, child.center() - ray.o)
+ * for the 8 children, then the std::sort above */
+static void travorder(const ora_scene *s, const onode *nd, const float r[8],
+                      int ord[8])
+{
+        float dist[8];
+        v3 o = vget(r), d = vget(r + 3);
+        for (int ci = 0; ci < 8; ++ci) {
+                const float *b = s->nodes[nd->child + ci].box;
+                v3 c = muls(add(vget(b), vget(b + 3)), .5f); /* center() */
+                dist[ci] = dot(d, sub(c, o));
+        }
+        ora_sort8(dist, ord);
 }
 
 static int ray_march(const ora_scene *s, const float r[8], omarch *m)

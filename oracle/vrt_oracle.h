@@ -61,6 +61,11 @@ void ora_make_ray(const float o[3], const float d[3], float tmin, float tmax,
 /* AABB3D::isect(ray, nullptr): VRT/graphics_math.h:1312-1332 */
 int ora_aabb_isect(const float box[6], const float ray[8]);
 
+/* travorder's std::sort of the 8 (ci, dist) Items and ray_march_isect's
+ * std::min_element, on arbitrary inputs (VRT/voxel_octree.cc:91-93,122-125) */
+void ora_sort8(const float dist[8], int ord[8]);
+int ora_first_min(const float *depth, int n);
+
 /* Scene: triangles as built by Triangle::Triangle (VRT/voxel_octree.cc:423-431).
  * pos: ntri*9, nrm: ntri*9 (raw, normalised here like the ctor), uv: ntri*6,
  * mat: ntri material ids.  Materials: mat_tex[m] = texture id or -1 (then

@@ -21,13 +21,20 @@ def pytest_configure(config):
 
 
 def _ensure_built():
+    """Build when a library is missing or libvrt.so's embedded source hash
+    (vrt_build_id) differs from the tree's: the tests must exercise the
+    sources at this HEAD, not a stale binary."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import build_id
     need = [os.path.join(ROOT, "voxelraytrace20190722_amd", "libvrt.so"),
             os.path.join(ROOT, "oracle", "liboracle.so")]
-    if all(os.path.exists(p) for p in need):
+    if all(os.path.exists(p) for p in need) and not build_id.stale():
         return
     if shutil.which("make") is None:
-        raise RuntimeError("libraries missing and `make` unavailable")
+        raise RuntimeError("libvrt.so missing or stale (build id) and `make` unavailable")
     subprocess.run(["make", "-j8"], cwd=ROOT, check=True)
+    if build_id.stale():
+        raise RuntimeError("libvrt.so build id still differs from the tree after make")
 
 
 _ensure_built()

@@ -161,6 +161,106 @@ def pcg_std():
             np.array([pts[s] for s in seeds], np.float32))
 
 
+def _ftok(x):
+    """float32 -> a token travorder_std.cpp reads back bit-exactly."""
+    x = np.float32(x)
+    if np.isnan(x):
+        return "nanx%08x" % int(np.array(x).view(np.uint32))
+    if np.isinf(x):
+        return "inf" if x > 0 else "-inf"
+    return float(x).hex()
+
+
+def travorder_cases(seed=20190722):
+    """Adversarial inputs for travorder's std::sort and ray_march_isect's
+    std::min_element: ties, +-0, +-inf, NaN (several payloads/signs, any
+    position), denormals, presorted / reversed runs, plus plain random."""
+    rng = np.random.default_rng(seed)
+    nan_bits = np.array([0x7fc00000, 0xffc00000, 0x7f800001, 0x7fc00123], np.uint32).view(np.float32)
+    special = np.concatenate([np.float32([0.0, -0.0, np.inf, -np.inf, 1.0, -1.0, 1e-45, -1e-45, 1.17549435e-38,
+                                          3.4028235e38, -3.4028235e38, 0.5, 0.5, 2.0]), nan_bits])
+    dist = []
+    for k in range(4096):
+        kind = k % 8
+        if kind == 0:
+            d = rng.normal(0, 1, 8)
+        elif kind == 1:  # heavy ties
+            d = rng.choice(np.float32([0.0, -0.0, 1.0, 1.0, 2.0]), 8)
+        elif kind == 2:  # specials everywhere
+            d = rng.choice(special, 8)
+        elif kind == 3:  # one or two NaNs in random positions, finite otherwise
+            d = rng.normal(0, 3, 8)
+            for _ in range(1 + (k // 8) % 2):
+                d[rng.integers(0, 8)] = rng.choice(nan_bits)
+        elif kind == 4:  # presorted / reversed / constant runs with ties
+            d = np.sort(rng.integers(-3, 4, 8).astype(np.float32))
+            d = d[::-1] if (k // 8) % 2 else d
+        elif kind == 5:  # denormals and signed zeros
+            d = rng.choice(np.float32([1e-45, 2e-45, -1e-45, 0.0, -0.0, 1e-40]), 8)
+        elif kind == 6:  # infinities among finite values
+            d = rng.normal(0, 1, 8)
+            d[rng.integers(0, 8, 3)] = rng.choice(np.float32([np.inf, -np.inf]), 3)
+        else:  # realistic: travorder distances of children of one box
+            c = rng.uniform(-1, 1, 3)
+            h = rng.uniform(0.01, 1)
+            o = rng.uniform(-2, 2, 3)
+            dd = rng.normal(0, 1, 3)
+            dd /= np.linalg.norm(dd)
+            d = [np.float32(dd[0]) * np.float32(c[0] + (h if ci & 4 else -h) - o[0])
+                 + np.float32(dd[1]) * np.float32(c[1] + (h if ci & 2 else -h) - o[1])
+                 + np.float32(dd[2]) * np.float32(c[2] + (h if ci & 1 else -h) - o[2]) for ci in range(8)]
+        dist.append(np.asarray(d, np.float32))
+    dist = np.array(dist, np.float32)
+    # hit masks: any, and ones with <= 2 / <= 4 children (the fast paths)
+    mask = rng.integers(0, 256, len(dist)).astype(np.uint32)
+    for k in range(len(dist)):
+        if k % 3 == 1:
+            mask[k] &= mask[k] - 1  # fewer bits
+            mask[k] &= rng.integers(0, 256)
+        elif k % 3 == 2:
+            bits = rng.choice(8, rng.integers(0, 3), replace=False)
+            mask[k] = np.uint32(sum(1 << int(b) for b in bits))
+    depth = np.zeros((2048, 16), np.float32)
+    length = np.zeros(2048, np.int32)
+    for j in range(2048):
+        n = j % 17
+        length[j] = n
+        kind = (j // 17) % 4
+        if kind == 0:
+            v = rng.uniform(0, 5, n)
+        elif kind == 1:
+            v = rng.choice(np.float32([1.0, 1.0, 2.0, 0.0, -0.0]), n)
+        elif kind == 2:
+            v = rng.choice(special, n)
+        else:
+            v = rng.uniform(0, 2, n).astype(np.float32)
+            if n:
+                v[rng.integers(0, n)] = rng.choice(nan_bits)
+        depth[j, :n] = v
+    return dist, mask, depth, length
+
+
+def travorder_std():
+    """The real libstdc++ std::sort / std::min_element on travorder_cases()
+    (tests/golden/travorder_std.cpp compiled with g++)."""
+    import subprocess
+    import tempfile
+    dist, mask, depth, length = travorder_cases()
+    lines = ["S " + " ".join(_ftok(x) for x in d) for d in dist]
+    lines += [f"M {n} " + " ".join(_ftok(x) for x in depth[j, :n]) for j, n in enumerate(length)]
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "travorder_std")
+        subprocess.run(["g++", "-O2", "-ffp-contract=off", "-o", exe, os.path.join(HERE, "travorder_std.cpp")],
+                       check=True)
+        out = subprocess.run([exe], input="\n".join(lines) + "\n", check=True, capture_output=True,
+                             text=True).stdout.splitlines()
+    order = np.array([[int(x) for x in ln.split()[1:]] for ln in out if ln[0] == "S"], np.int32)
+    argmin = np.array([int(ln.split()[1]) for ln in out if ln[0] == "M"], np.int32)
+    assert order.shape == (len(dist), 8) and argmin.shape == (len(length),)
+    np.savez_compressed(os.path.join(HERE, "travorder_std.npz"), dist=dist, mask=mask, order=order,
+                        depth=depth, length=length, argmin=argmin)
+
+
 def secondary_fixture(sd, depth, cam, film, spp, name):
     osc = po.Scene(sd, depth)
     c = po.camera(*cam)
@@ -210,6 +310,10 @@ def main():
     if sys.argv[1:] == ["ingest"]:
         ingest_fixture()
         return
+    if sys.argv[1:] == ["travorder"]:
+        travorder_std()
+        return
+    travorder_std()
     ingest_fixture()
     q, out = kat_raytri()
     np.savez_compressed(os.path.join(HERE, "kat_raytri.npz"), inp=q, out=out)

@@ -291,3 +291,25 @@ def test_scene_nodes_and_build_flags():
     assert np.array_equal(a[internal], 1 + 8 * np.arange(len(internal)))
     with pytest.raises(vrt.VrtError):
         vrt.VoxelOctree(sd, 6, device=-1, build_on_device=True)
+
+
+def test_build_id_matches_tree():
+    """libvrt.so was built from the sources in this tree (tools/build_id.py)."""
+    import build_id
+    assert vrt.build_id() == build_id.compute()
+
+
+def test_stbi_write_hdr_is_the_reference_entry_point(tmp_path):
+    """stbi_write_hdr under its own name (VRT/stb_image_write.h:178): a
+    reference caller relinks without renaming the call; same bytes as the
+    reference writer's fixture."""
+    z = golden("hdr_ref.npz")
+    for i in range(3):
+        img = np.ascontiguousarray(z[f"img{i}"], np.float32)
+        h, w = img.shape[:2]
+        comp = 1 if img.ndim == 2 else img.shape[2]
+        p = tmp_path / f"s{i}.hdr"
+        assert vrt.lib().stbi_write_hdr(str(p).encode(), w, h, comp, img.ctypes.data_as(vrt._ffi.f32p)) == 1
+        assert p.read_bytes() == z[f"bytes{i}"].tobytes(), i
+    assert vrt.lib().stbi_write_hdr(str(tmp_path / "no" / "x.hdr").encode(), 1, 1, 3,
+                                    np.zeros(3, np.float32).ctypes.data_as(vrt._ffi.f32p)) == 0

@@ -82,3 +82,16 @@ def test_oracle_secondary_matches_fixture():
     assert np.array_equal(vis.view(np.uint32), z["vis"].view(np.uint32))
     for k in ("hit", "tri", "voxel"):
         assert np.array_equal(d[k], z[k])
+
+
+def test_oracle_travorder_matches_libstdcxx_sort():
+    """travorder's std::sort of the 8 Items (VRT/voxel_octree.cc:91-93) and
+    ray_march_isect's std::min_element (:122-125): the oracle's restatement
+    == the real libstdc++ calls (tests/golden/travorder_std.cpp) on ties,
+    +-0, +-inf, NaN and denormal inputs."""
+    z = golden("travorder_std.npz")
+    assert np.isnan(z["dist"]).any(1).sum() > 500  # the NaN cases are there
+    for d, o in zip(z["dist"], z["order"]):
+        assert np.array_equal(po.sort8(d), o)
+    for dep, n, k in zip(z["depth"], z["length"], z["argmin"]):
+        assert po.first_min(dep[:n]) == k

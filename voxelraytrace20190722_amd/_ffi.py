@@ -116,6 +116,10 @@ SIGNATURES = {
     "vrt_ray_march_batch_device": (C.c_int, [_P, _P, C.c_int64, _P, _P]),
     "vrt_device_selftest": (C.c_int, [C.c_int, f64p, f64p, f32p, i32p, C.c_int64]),
     "vrt_write_hdr": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, f32p]),
+    "stbi_write_hdr": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, f32p]),
+    "vrt_build_id": (C.c_char_p, []),
+    "vrt_device_selftest_order": (C.c_int, [C.c_int, f32p, u32p, C.c_int64, u32p, f32p, i32p, C.c_int64,
+                                            C.c_int32, i32p]),
     "vrt_write_hdr_mem": (C.c_int64, [C.c_int, C.c_int, C.c_int, f32p, u8p, C.c_int64]),
     "vrt_rgbe_device": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P]),
     "vrt_write_hdr_rgbe": (C.c_int, [C.c_char_p, C.c_int, C.c_int, u8p]),

@@ -549,6 +549,33 @@ def sweep_pose(root_min, root_max, i, n):
     return fov.value, eye, spot, up
 
 
+def device_selftest_order(dist, hit_mask, depth=None, lengths=None, device=0):
+    """The kernels' travorder sort and min_element code on arbitrary inputs
+    (vrt_device_selftest_order): dist (n, 8) f32, hit_mask (n,) -> (n, 6)
+    u32 order words; depth (m, k) f32 + lengths (m,) -> (m,) first argmin."""
+    dist = np.ascontiguousarray(np.asarray(dist, np.float32).reshape(-1, 8))
+    hm = np.ascontiguousarray(np.asarray(hit_mask, np.uint32).reshape(-1))
+    n = dist.shape[0]
+    assert hm.shape[0] == n
+    orders = np.zeros((n, 6), np.uint32)
+    m, stride, dep, ln, am = 0, 0, None, None, None
+    if depth is not None:
+        dep = np.ascontiguousarray(np.asarray(depth, np.float32))
+        m, stride = dep.shape
+        ln = np.ascontiguousarray(np.asarray(lengths, np.int32).reshape(-1))
+        assert ln.shape[0] == m
+        am = np.zeros(m, np.int32)
+    check(lib().vrt_device_selftest_order(device, ptr(dist, _ffi.f32p), ptr(hm, _ffi.u32p), n,
+                                          ptr(orders, _ffi.u32p), ptr(dep, _ffi.f32p), ptr(ln, _ffi.i32p), m,
+                                          stride, ptr(am, _ffi.i32p)), "vrt_device_selftest_order")
+    return orders, am
+
+
+def build_id():
+    """Source hash libvrt.so was built from (tools/build_id.py)."""
+    return lib().vrt_build_id().decode()
+
+
 def device_count():
     n = C.c_int32()
     check(lib().vrt_device_count(C.byref(n)), "vrt_device_count")

@@ -234,3 +234,9 @@ extern "C" int vrt_write_hdr(const char *filename, int w, int h, int comp,
                 return 0;
         return to_file(o, filename);
 }
+
+// the reference's own entry point (VRT/stb_image_write.h:178): same writer
+extern "C" int stbi_write_hdr(char const *filename, int w, int h, int comp, const float *data)
+{
+        return vrt_write_hdr(filename, w, h, comp, data);
+}

@@ -330,6 +330,21 @@ struct vrt_scene {
         hipStream_t stream = nullptr;
         hipEvent_t ev0 = nullptr, ev1 = nullptr;
         bool timed = false;
+        // persistent-render work queues (WorkQueue, vrt_internal.h): a ring
+        // of kQueueSlots counter sets, each with its bases and the event of
+        // its last launch
+        uint32_t *d_queue = nullptr;
+        uint32_t q_base[kQueueSlots][8] = {};
+        hipEvent_t q_ev[kQueueSlots] = {};
+        bool q_live[kQueueSlots] = {};
+        int q_next = 0;
+        // scene-owned device scratch (light map, split-trace records): the
+        // event of the last launch that used it
+        hipEvent_t scratch_ev = nullptr;
+        bool scratch_live = false;
+        // every entry point that launches work on the scene holds mu (one
+        // host thread at a time; device work on several streams is ordered
+        // by the events above)
         std::mutex mu;
 };
 
@@ -630,7 +645,8 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         const size_t sz_tex = (size_t)std::max<int64_t>(16, s->tex_bytes);
         size_t off[10];
         size_t tot = 0;
-        const size_t sizes[9] = { sz_nodes, sz_vox, sz_refs, sz_pos, sz_attr, sz_mats, sz_texs, sz_tex, kCtrBytes };
+        const size_t sizes[9] = { sz_nodes, sz_vox, sz_refs, sz_pos, sz_attr, sz_mats, sz_texs, sz_tex,
+                                  kQueueSlots * kQueueBytes };
         for (int i = 0; i < 9; ++i) {
                 off[i] = tot;
                 tot += align_up(sizes[i]);
@@ -638,7 +654,7 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         off[9] = tot;
         HIPCHK(hipMalloc(&s->d_mem, tot));
         char *base = static_cast<char *>(s->d_mem);
-        HIPCHK(hipMemset(base + off[8], 0, kCtrBytes));
+        HIPCHK(hipMemset(base + off[8], 0, kQueueSlots * kQueueBytes));
         HIPCHK(hipMemcpy(base + off[0], s->nodes.data(), sz_nodes, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(base + off[1], s->node_vox.data(), sz_vox, hipMemcpyHostToDevice));
         if (refs_bytes)
@@ -660,7 +676,8 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         s->dev.mats = reinterpret_cast<const MatRec *>(base + off[5]);
         s->dev.texs = reinterpret_cast<const TexRec *>(base + off[6]);
         s->dev.tex_data = reinterpret_cast<const uint8_t *>(base + off[7]);
-        s->dev.ctr = reinterpret_cast<uint32_t *>(base + off[8]);
+        s->d_queue = reinterpret_cast<uint32_t *>(base + off[8]);
+        HIPCHK(persistent_render_blocks(&s->dev.persist_blocks));
         s->dev.max_depth = s->max_depth;
         s->dev.nmat = (int32_t)s->mats.size();
         s->dev.ntex = (int32_t)s->texs.size();
@@ -677,6 +694,9 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreate(&s->ev0));
         HIPCHK(hipEventCreate(&s->ev1));
+        for (int k = 0; k < kQueueSlots; ++k)
+                HIPCHK(hipEventCreateWithFlags(&s->q_ev[k], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&s->scratch_ev, hipEventDisableTiming));
         return VRT_OK;
 }
 
@@ -797,7 +817,7 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
 {
         if (!s)
                 return;
-        if (s->d_mem || s->d_lm || s->d_light || s->d_trace || s->stream || s->ev0 || s->ev1) {
+        if (s->d_mem || s->d_lm || s->d_light || s->d_trace || s->stream || s->ev0 || s->ev1 || s->scratch_ev) {
                 (void)hipSetDevice(s->device);
                 if (s->stream)
                         (void)hipStreamSynchronize(s->stream);
@@ -813,6 +833,11 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                         (void)hipEventDestroy(s->ev0);
                 if (s->ev1)
                         (void)hipEventDestroy(s->ev1);
+                for (int k = 0; k < kQueueSlots; ++k)
+                        if (s->q_ev[k])
+                                (void)hipEventDestroy(s->q_ev[k]);
+                if (s->scratch_ev)
+                        (void)hipEventDestroy(s->scratch_ev);
                 if (s->stream)
                         (void)hipStreamDestroy(s->stream);
         }
@@ -909,6 +934,55 @@ static void fill_render_params(vrt_scene *s, const vrt_camera *cam,
         p->tiles_this_rank = rank < T ? (T - rank + nranks - 1) / nranks : 0;
 }
 
+// One render launch on stream st (caller holds s->mu).  A persistent launch
+// takes the next work-queue slot of the scene's ring: st first waits for the
+// slot's previous launch (on whatever stream it ran), the kernel takes its
+// units from base[] on, and the slot's bases advance by exactly the adds the
+// launch makes (WorkQueue, vrt_internal.h).
+static int render_launch(vrt_scene *s, RenderParams &p, bool instrumented, hipStream_t st)
+{
+        int slot = -1;
+        if (render_uses_queue(p.sc, instrumented)) {
+                slot = s->q_next;
+                s->q_next = (slot + 1) % kQueueSlots;
+                if (s->q_live[slot])
+                        HIPCHK(hipStreamWaitEvent(st, s->q_ev[slot], 0));
+                p.q.ctr = s->d_queue + (size_t)slot * (kQueueBytes / sizeof(uint32_t));
+                std::memcpy(p.q.base, s->q_base[slot], sizeof p.q.base);
+        }
+        int waves = 0;
+        HIPCHK(launch_render(p, instrumented, st, &waves));
+        if (slot >= 0 && waves > 0) {
+                const int units = p.tiles_this_rank * 4;
+                for (int x = 0; x < 8; ++x) {
+                        int lo, hi;
+                        queue_range(units, x, lo, hi);
+                        if (hi > lo)
+                                s->q_base[slot][x] += (uint32_t)(hi - lo) + (uint32_t)waves;
+                }
+                HIPCHK(hipEventRecord(s->q_ev[slot], st));
+                s->q_live[slot] = true;
+        }
+        return VRT_OK;
+}
+
+// Scene-owned scratch (light map, split-trace records) serves one launch at
+// a time: the next user's stream waits for the previous user's (caller
+// holds s->mu).
+static int scratch_acquire(vrt_scene *s, hipStream_t st)
+{
+        if (s->scratch_live)
+                HIPCHK(hipStreamWaitEvent(st, s->scratch_ev, 0));
+        return VRT_OK;
+}
+
+static int scratch_release(vrt_scene *s, hipStream_t st)
+{
+        HIPCHK(hipEventRecord(s->scratch_ev, st));
+        s->scratch_live = true;
+        return VRT_OK;
+}
+
 extern "C" int vrt_render_tiles_device(vrt_scene *s, const vrt_camera *cam,
                                        const vrt_film *film, int rank,
                                        int nranks, int image_layout,
@@ -924,6 +998,7 @@ extern "C" int vrt_render_tiles_device(vrt_scene *s, const vrt_camera *cam,
                 return fail(VRT_E_INVALID, "rank %d of %d", rank, nranks);
         if (image_layout && nranks != 1)
                 return fail(VRT_E_INVALID, "image_layout requires nranks == 1");
+        std::lock_guard<std::mutex> lk(s->mu);
         HIPCHK(hipSetDevice(s->device));
         RenderParams p;
         fill_render_params(s, cam, film, rank, nranks, &p);
@@ -931,7 +1006,8 @@ extern "C" int vrt_render_tiles_device(vrt_scene *s, const vrt_camera *cam,
         p.out = d_out;
         hipStream_t st = static_cast<hipStream_t>(stream);
         HIPCHK(hipEventRecord(s->ev0, st));
-        HIPCHK(launch_render(p, false, st));
+        if (int rc = render_launch(s, p, false, st))
+                return rc;
         HIPCHK(hipEventRecord(s->ev1, st));
         s->timed = true;
         return VRT_OK;
@@ -941,6 +1017,7 @@ extern "C" int vrt_last_kernel_ms(vrt_scene *s, float *ms)
 {
         if (!s || !ms)
                 return fail(VRT_E_INVALID, "null argument");
+        std::lock_guard<std::mutex> lk(s->mu);
         if (!s->timed)
                 return fail(VRT_E_INVALID, "no timed launch yet");
         HIPCHK(hipSetDevice(s->device));
@@ -1031,7 +1108,8 @@ extern "C" int vrt_render(vrt_scene *s, const vrt_camera *cam,
                 p.so.cnt = static_cast<uint32_t *>(scnt.p);
         }
         HIPCHK(hipEventRecord(s->ev0, s->stream));
-        HIPCHK(launch_render(p, want_cnt, s->stream));
+        if (int rc = render_launch(s, p, want_cnt, s->stream))
+                return rc;
         HIPCHK(hipEventRecord(s->ev1, s->stream));
         s->timed = true;
         HIPCHK(hipStreamSynchronize(s->stream));
@@ -1097,6 +1175,7 @@ extern "C" int vrt_render_secondary_device(vrt_scene *s, const vrt_camera *cam,
                 return rc;
         if (nranks < 1 || rank < 0 || rank >= nranks)
                 return fail(VRT_E_INVALID, "rank %d of %d", rank, nranks);
+        std::lock_guard<std::mutex> lk(s->mu);
         HIPCHK(hipSetDevice(s->device));
         RenderParams p;
         fill_render_params(s, cam, film, 0, 1, &p);
@@ -1249,6 +1328,8 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
                                  (size_t)nnodes * (sizeof(LMRec) + sizeof(float4)) + 256));
         float4 *d_cc = reinterpret_cast<float4 *>(s->d_lm + nnodes);
         uint32_t *d_bad = reinterpret_cast<uint32_t *>(d_cc + nnodes);
+        if (int rc = scratch_acquire(s, s->stream))  // a trace render may still read the light map
+                return rc;
         HIPCHK(hipMemsetAsync(s->d_lm, 0, (size_t)nnodes * sizeof(LMRec), s->stream));
         HIPCHK(hipMemsetAsync(d_bad, 0, 4, s->stream));
         // scratch: keys/vals in+out, per-sample (illum, normal), sort temp
@@ -1301,6 +1382,8 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         s->timed = true;
         unsigned long long h = 0;
         HIPCHK(hipMemcpyAsync(&h, d_hits, sizeof h, hipMemcpyDeviceToHost, s->stream));
+        if (int rc = scratch_release(s, s->stream))
+                return rc;
         HIPCHK(hipStreamSynchronize(s->stream));
         if (hits)
                 *hits = (int64_t)h;
@@ -1416,6 +1499,7 @@ extern "C" int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam, cons
                 return fail(VRT_E_INVALID, "image_layout requires nranks == 1");
         if (int rc = trace_ok(s, min_voxel))
                 return rc;
+        std::lock_guard<std::mutex> lk(s->mu);
         HIPCHK(hipSetDevice(s->device));
         TraceParams tp0, tp;
         fill_trace_params(s, cam, film, min_voxel, rank, nranks, &tp0);
@@ -1424,9 +1508,13 @@ extern "C" int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam, cons
         hipStream_t st = static_cast<hipStream_t>(stream);
         if (int rc = trace_scratch(s, tp0, &tp, st))
                 return rc;
+        if (int rc = scratch_acquire(s, st))
+                return rc;
         HIPCHK(hipEventRecord(s->ev0, st));
         HIPCHK(launch_trace(tp, st));
         HIPCHK(hipEventRecord(s->ev1, st));
+        if (int rc = scratch_release(s, st))
+                return rc;
         s->timed = true;
         return VRT_OK;
 }
@@ -1466,9 +1554,13 @@ extern "C" int vrt_render_trace(vrt_scene *s, const vrt_camera *cam, const vrt_f
                 HIPCHK(hipMemsetAsync(dr.p, 0, ns * 12, s->stream));
                 tp.r.so.rgb = static_cast<float *>(dr.p);
         }
+        if (int rc = scratch_acquire(s, s->stream))
+                return rc;
         HIPCHK(hipEventRecord(s->ev0, s->stream));
         HIPCHK(launch_trace(tp, s->stream));
         HIPCHK(hipEventRecord(s->ev1, s->stream));
+        if (int rc = scratch_release(s, s->stream))
+                return rc;
         s->timed = true;
         HIPCHK(hipStreamSynchronize(s->stream));
         HIPCHK(hipMemcpy(rgb, img.p, npix * 12, hipMemcpyDeviceToHost));
@@ -1542,5 +1634,47 @@ extern "C" int vrt_device_selftest(int device, const double *mt_in,
                 HIPCHK(hipMemcpy(mt_out, b.p, (size_t)n * 4 * 8, hipMemcpyDeviceToHost));
         if (sat_in)
                 HIPCHK(hipMemcpy(sat_out, d.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+        return VRT_OK;
+}
+
+extern "C" int vrt_device_selftest_order(int device, const float *dist, const uint32_t *hit_mask, int64_t n,
+                                         uint32_t *orders, const float *depth, const int32_t *len, int64_t m,
+                                         int32_t stride, int32_t *argmin)
+{
+        if (n < 0 || m < 0 || (n > 0 && (!dist || !hit_mask || !orders)) ||
+            (m > 0 && (!depth || !len || !argmin || stride < 0)))
+                return fail(VRT_E_INVALID, "bad argument");
+        for (int64_t j = 0; j < m; ++j)
+                if (len[j] < 0 || len[j] > stride)
+                        return fail(VRT_E_INVALID, "record list %lld: length %d outside [0, %d]", (long long)j,
+                                    len[j], stride);
+        if (int rc = check_device(device))
+                return rc;
+        HIPCHK(hipSetDevice(device));
+        DevBuf dd, dh, dout, ddep, dlen, darg;
+        if (n > 0) {
+                HIPCHK(hipMalloc(&dd.p, (size_t)n * 8 * sizeof(float)));
+                HIPCHK(hipMalloc(&dh.p, (size_t)n * sizeof(uint32_t)));
+                HIPCHK(hipMalloc(&dout.p, (size_t)n * 6 * sizeof(uint32_t)));
+                HIPCHK(hipMemcpy(dd.p, dist, (size_t)n * 8 * sizeof(float), hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(dh.p, hit_mask, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
+        if (m > 0) {
+                HIPCHK(hipMalloc(&ddep.p, std::max<size_t>(1, (size_t)m * stride) * sizeof(float)));
+                HIPCHK(hipMalloc(&dlen.p, (size_t)m * sizeof(int32_t)));
+                HIPCHK(hipMalloc(&darg.p, (size_t)m * sizeof(int32_t)));
+                if (stride > 0)
+                        HIPCHK(hipMemcpy(ddep.p, depth, (size_t)m * stride * sizeof(float), hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(dlen.p, len, (size_t)m * sizeof(int32_t), hipMemcpyHostToDevice));
+        }
+        HIPCHK(launch_selftest_order(static_cast<float *>(dd.p), static_cast<uint32_t *>(dh.p), n,
+                                     static_cast<uint32_t *>(dout.p), static_cast<float *>(ddep.p),
+                                     static_cast<int32_t *>(dlen.p), m, stride, static_cast<int32_t *>(darg.p),
+                                     nullptr));
+        HIPCHK(hipDeviceSynchronize());
+        if (n > 0)
+                HIPCHK(hipMemcpy(orders, dout.p, (size_t)n * 6 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (m > 0)
+                HIPCHK(hipMemcpy(argmin, darg.p, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost));
         return VRT_OK;
 }

@@ -88,11 +88,36 @@ struct DevScene {
         int32_t fast_ok;  // root box finite and |coords| < 2^60 (expand_v1, fast_ok())
         int32_t wide_leaves;  // >= 8 records per non-empty leaf on average: RefRec64 records,
                               // wave-uniform leaf loads (leaf_isect)
-        uint32_t *ctr;        // k_render_p work counters: [x * kCtrStride], x = 0..7 per XCD,
-                              // 8 = finished waves; zero between launches
+        int32_t persist_blocks;  // resident 256-thread blocks of the persistent render on this
+                                 // device (a multiple of 8), 0 = no persistent launches
 };
-constexpr int kCtrStride = 32;  // one 128-B line per counter
-constexpr size_t kCtrBytes = 9 * kCtrStride * sizeof(uint32_t);
+
+// Work queue of one persistent launch (k_render_p): 8 counters, one per XCD
+// slice of the units, one 128-B line each.  The kernel never resets them:
+// unit j of slice x is taken by the atomicAdd that returns base[x] + j, and
+// every wave makes exactly one more (failing) add per non-empty slice, so
+// after a launch of `waves` waves counter x has advanced by
+// (hi - lo of queue_range(units, x)) + waves -- the host keeps base[] from that, per ring
+// slot (vrt_host.cpp: take_queue / release_queue).  Launches on different
+// streams use different slots; a slot is reused only after its previous
+// launch has finished (an event), so no two launches share counters and no
+// memset is needed.
+constexpr int kQueueStride = 32;
+constexpr int kQueueSlots = 8;
+constexpr size_t kQueueBytes = 8 * kQueueStride * sizeof(uint32_t);
+struct WorkQueue {
+        uint32_t *ctr;
+        uint32_t base[8];
+};
+// units of slice x: a contiguous range [lo, hi) of the unit order
+__host__ __device__ inline void queue_range(int units, int x, int &lo, int &hi)
+{
+        const int per = (units + 7) >> 3;
+        lo = x * per;
+        hi = lo + per < units ? lo + per : units;
+        if (hi < lo)
+                hi = lo;
+}
 
 // Camera + film constants for ray generation (T1), computed on the host.
 struct CamParams {
@@ -121,6 +146,7 @@ struct RenderParams {
         int32_t image_layout;  // 1: out is nx*ny*3 image; 0: packed tiles
         float *out;
         SampleOut so;
+        WorkQueue q;           // persistent launches only
 };
 
 // ---- full trace() -------------------------------------
@@ -179,8 +205,13 @@ hipError_t build_tree_device(int device, const float *pos, int ntri, const float
                              const float root_mx[3], int max_depth, DeviceBuild *out, std::string *err);
 
 // Kernel launchers (vrt_kernels.hip)
+// true when launch_render runs the persistent kernel, which takes its units
+// from p.q; *queue_waves = the waves launched (for the queue bases)
+bool render_uses_queue(const DevScene &sc, bool instrumented);
 hipError_t launch_render(const RenderParams &p, bool instrumented,
-                         hipStream_t st);
+                         hipStream_t st, int *queue_waves);
+// resident blocks of the persistent render on the current device
+hipError_t persistent_render_blocks(int *blocks);
 hipError_t launch_ray_march(const DevScene &sc, const void *d_rays,
                             int64_t n, void *d_hits, hipStream_t st);
 hipError_t launch_unpack(int nx, int ny, int ntx, int nty, int nranks,
@@ -208,6 +239,9 @@ hipError_t sort_pairs_u32(void *temp, size_t *temp_bytes, const uint32_t *keys_i
                           const uint32_t *vals_in, uint32_t *vals_out, int64_t n, int bits, hipStream_t st);
 hipError_t launch_iota(uint32_t *v, int64_t n, hipStream_t st);
 hipError_t launch_rgbe(const float *img, int64_t npx, int comp, uint8_t *out, hipStream_t st);
+hipError_t launch_selftest_order(const float *dist, const uint32_t *hm, int64_t n, uint32_t *out,
+                                 const float *depth, const int32_t *len, int64_t m, int32_t stride,
+                                 int32_t *argmin, hipStream_t st);
 hipError_t launch_selftest(const double *mt_in, double *mt_out,
                            const float *sat_in, int32_t *sat_out, int64_t n,
                            hipStream_t st);

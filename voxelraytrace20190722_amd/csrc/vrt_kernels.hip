@@ -48,9 +48,171 @@ __device__ __forceinline__ void load_node(const NodeRec *__restrict__ nodes,
         b = __float_as_uint(q1.w);
 }
 
-#ifndef VRT_EXPAND_V
-#define VRT_EXPAND_V 2
-#endif
+// ---------------------------------------------------------------------------
+// travorder's child order (VRT/voxel_octree.cc:77-97): std::sort of the 8
+// Items {ci, dist} with `lhs.dist < rhs.dist`.  For 8 elements libstdc++'s
+// std::sort is one __insertion_sort (the introsort loop stops at 16
+// elements): move-to-front when val < first, else __unguarded_linear_insert
+// (shift while val < prev).  With no NaN among the distances that is the
+// stable order on (dist, ci); a NaN dist breaks the total order, and only the
+// insertion sort itself reproduces the result.  The kernel keeps only the
+// children whose slab test passed (hm), in that order, 3 bits each (first
+// child in bits 0-2).  These helpers are the kernel's own sort code, called
+// by expand_* below and by k_selftest_order, which pins them against the
+// real libstdc++ std::sort (tests/golden/travorder_std.cpp).
+// ---------------------------------------------------------------------------
+
+// The insertion sort itself on a packed permutation word (3-bit field p =
+// child at position p), as adjacent swaps of val from position j to j-1:
+// all of them when val < a[0], else until the first failing comparison.
+// dist_of(ci) returns child ci's distance (recomputed per use: few live
+// registers on this rare path).
+template <class DistOf>
+__device__ __forceinline__ uint32_t insertion_perm8(DistOf dist_of)
+{
+        uint32_t perm = 0xFAC688u;  // position p holds child p
+#pragma unroll
+        for (int i = 1; i < 8; ++i) {
+                const uint32_t vi = (perm >> (3 * i)) & 7u;
+                const float v = dist_of(vi);
+                const bool front = v < dist_of(perm & 7u);
+                bool go = true;
+#pragma unroll
+                for (int j = i; j >= 1; --j) {
+                        const uint32_t pk = (perm >> (3 * (j - 1))) & 7u;
+                        go = go && (front || v < dist_of(pk));
+                        const uint32_t sw = (perm & ~(63u << (3 * (j - 1)))) | (pk << (3 * j)) |
+                                            (vi << (3 * (j - 1)));
+                        perm = go ? sw : perm;
+                }
+        }
+        return perm;
+}
+
+// The hit children of a full order `perm`, in order; n = their number;
+// full_pos (kFullPos) = the position of each child ci in the full order,
+// bits 3ci (the reference's test counts).
+template <bool kFullPos>
+__device__ __forceinline__ uint32_t perm_filter(uint32_t perm, uint32_t hm, int &n, uint32_t &full_pos)
+{
+        uint32_t order = 0;
+        int k = 0;
+        full_pos = 0;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+                const uint32_t ci = (perm >> (3 * p)) & 7u;
+                const bool hc = (hm >> ci) & 1u;
+                order |= hc ? (ci << (3 * k)) : 0u;
+                k += hc ? 1 : 0;
+                if (kFullPos)
+                        full_pos |= (uint32_t)p << (3 * ci);
+        }
+        n = k;
+        return order;
+}
+
+// No NaN: the rank of each hit child among the hit children under the
+// stable (dist, index) order (j < i precedes i <=> !(dist_i < dist_j));
+// full_pos (kFullPos) = rank among all 8.
+template <bool kFullPos>
+__device__ __forceinline__ uint32_t rank_order8(const float dist[8], uint32_t hm, uint32_t &full_pos)
+{
+        uint32_t rk[8], fp[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+                rk[i] = 0;
+                fp[i] = 0;
+        }
+#pragma unroll
+        for (int i = 1; i < 8; ++i) {
+#pragma unroll
+                for (int j = 0; j < i; ++j) {
+                        const bool c = dist[i] < dist[j];  // i strictly first
+                        rk[j] += (uint32_t)(c & ((hm >> i) & 1u));
+                        rk[i] += (uint32_t)(!c & ((hm >> j) & 1u));
+                        if (kFullPos) {
+                                fp[j] += (uint32_t)c;
+                                fp[i] += (uint32_t)!c;
+                        }
+                }
+        }
+        uint32_t order = 0;
+        full_pos = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+                order |= ((hm >> i) & 1u) ? ((uint32_t)i << (3 * rk[i])) : 0u;
+                if (kFullPos)
+                        full_pos |= fp[i] << (3 * i);
+        }
+        return order;
+}
+
+// No NaN, at most 2 hit children: one comparator (ties keep index order,
+// i0 < i1).
+template <class DistOf>
+__device__ __forceinline__ uint32_t two_slot_order(DistOf dist_of, uint32_t hm)
+{
+        const uint32_t i0 = (uint32_t)__builtin_ctz(hm | 0x100u);
+        const uint32_t m1 = hm & (hm - 1u);
+        const uint32_t i1 = (uint32_t)__builtin_ctz(m1 | 0x100u);
+        const float d0 = dist_of(i0);
+        const float d1 = i1 < 8u ? dist_of(i1) : __int_as_float(0x7f800000);
+        const bool sw = d1 < d0;
+        return sw ? ((i1 & 7u) | ((i0 & 7u) << 3)) : ((i0 & 7u) | ((i1 & 7u) << 3));
+}
+
+__device__ __forceinline__ void ce4(float &da, uint32_t &ia, float &db, uint32_t &ib)
+{
+        const bool sw = (db < da) | ((db == da) & (ib < ia));
+        const float td = da;
+        const uint32_t ti = ia;
+        da = sw ? db : da;
+        ia = sw ? ib : ia;
+        db = sw ? td : db;
+        ib = sw ? ti : ib;
+}
+
+__device__ __forceinline__ void ce4_lt(float &da, uint32_t &ia, float &db, uint32_t &ib)
+{
+        const bool sw = db < da;
+        const float td = da;
+        const uint32_t ti = ia;
+        da = sw ? db : da;
+        ia = sw ? ib : ia;
+        db = sw ? td : db;
+        ib = sw ? ti : ib;
+}
+
+// No NaN, at most 4 hit children (a line through the 8 octants of a box
+// crosses at most 4, barring degenerate boxes): the children go into 4
+// slots in index order (empty slots sort last) and a 5-comparator network
+// orders them on the total order (dist, index).  The slots start in index
+// order, so in the first two layers the element in the lower slot always
+// has the lower index ((0,1),(2,3) trivially; (0,2),(1,3) compare a
+// slot-{0,1} child with a slot-{2,3} one): ties keep the order and the
+// comparison reduces to dist.  Only the last comparator (1,2) needs the
+// index.
+template <class DistOf>
+__device__ __forceinline__ uint32_t net4_order(DistOf dist_of, uint32_t hm)
+{
+        float d[4];
+        uint32_t id[4];
+        uint32_t m = hm;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+                const uint32_t i = m ? (uint32_t)__builtin_ctz(m) : 8u;
+                m &= m - 1u;
+                const float dv = dist_of(i);
+                d[k] = i < 8u ? dv : __int_as_float(0x7f800000);
+                id[k] = i;
+        }
+        ce4_lt(d[0], id[0], d[1], id[1]);
+        ce4_lt(d[2], id[2], d[3], id[3]);
+        ce4_lt(d[0], id[0], d[2], id[2]);
+        ce4_lt(d[1], id[1], d[3], id[3]);
+        ce4(d[1], id[1], d[2], id[2]);
+        return (id[0] & 7u) | ((id[1] & 7u) << 3) | ((id[2] & 7u) << 6) | ((id[3] & 7u) << 9);
+}
 
 // Expand an internal node with box [bmin,bmax]: slab-test its 8 children
 // (boxes from split()'s exact arithmetic) and return the hit children in
@@ -107,8 +269,7 @@ __device__ __forceinline__ uint32_t expand_v1(const float bmin[3],
                 q[k][1] = dd[k] * ((b + c) * .5f - oo[k]);
         }
         const float qx0 = 0.0f + q[0][0], qx1 = 0.0f + q[0][1];
-        float dist[8];
-        bool hit[8];
+        uint32_t hm = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
                 const int mx = (i >> 2) & 1, my = (i >> 1) & 1, mz = i & 1;
@@ -126,128 +287,33 @@ __device__ __forceinline__ uint32_t expand_v1(const float bmin[3],
                 }
                 // !(t0 > t1) && (t0 in [tmin,tmax] || t1 in [tmin,tmax]),
                 // evaluated without branches
-                hit[i] = ((content >> i) & 1u) & !(t0 > t1) & (((t0 >= r.tmin) & (t0 <= r.tmax)) |
-                                       ((t1 >= r.tmin) & (t1 <= r.tmax)));
-                dist[i] = ((mx ? qx1 : qx0) + q[1][my]) + q[2][mz];
+                const bool h = ((content >> i) & 1u) & !(t0 > t1) & (((t0 >= r.tmin) & (t0 <= r.tmax)) |
+                                                                     ((t1 >= r.tmin) & (t1 <= r.tmax)));
+                hm |= (uint32_t)h << i;
         }
-        if (!kFast) {
-                // exact path: libstdc++'s __insertion_sort itself (the ranks
-                // below assume a total order, which a NaN dist breaks):
-                // if (val < first) move_backward + put val first, else
-                // __unguarded_linear_insert (shift while val < prev) -- as
-                // adjacent swaps of val from position j to j-1: all of them
-                // when val < a[0], else until the first failing comparison.
-                // The permutation is one word of 3-bit fields; a child's
-                // dist is recomputed from its index with the same float ops
-                // (few live registers on this rare path).
-                auto dist_of = [&](uint32_t ci) {
-                        return (((ci & 4u) ? qx1 : qx0) + ((ci & 2u) ? q[1][1] : q[1][0])) +
-                               ((ci & 1u) ? q[2][1] : q[2][0]);
-                };
-                uint32_t perm = 0xFAC688u;  // position p holds child p
+        // travorder: dot(d, center - o), center = (min + max) * .5f, summed
+        // x + y + z from 0
+        auto dist_of = [&](uint32_t ci) {
+                return (((ci & 4u) ? qx1 : qx0) + ((ci & 2u) ? q[1][1] : q[1][0])) +
+                       ((ci & 1u) ? q[2][1] : q[2][0]);
+        };
+        if (!kFast)
+                return perm_filter<kFullPos>(insertion_perm8(dist_of), hm, cnt, full_pos);
+        float dist[8];
 #pragma unroll
-                for (int i = 1; i < 8; ++i) {
-                        const uint32_t vi = (perm >> (3 * i)) & 7u;
-                        const float v = dist_of(vi);
-                        const bool front = v < dist_of(perm & 7u);
-                        bool go = true;
-#pragma unroll
-                        for (int j = i; j >= 1; --j) {
-                                const uint32_t pk = (perm >> (3 * (j - 1))) & 7u;
-                                go = go && (front || v < dist_of(pk));
-                                const uint32_t sw = (perm & ~(63u << (3 * (j - 1)))) | (pk << (3 * j)) |
-                                                    (vi << (3 * (j - 1)));
-                                perm = go ? sw : perm;
-                        }
-                }
-                uint32_t hm = 0, order = 0;
-                int n = 0;
-                full_pos = 0;
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-                        hm |= (uint32_t)hit[i] << i;
-#pragma unroll
-                for (int p = 0; p < 8; ++p) {
-                        const uint32_t ci = (perm >> (3 * p)) & 7u;
-                        const bool hc = (hm >> ci) & 1u;
-                        order |= hc ? (ci << (3 * n)) : 0u;
-                        n += hc ? 1 : 0;
-                        if (kFullPos)
-                                full_pos |= (uint32_t)p << (3 * ci);
-                }
-                cnt = n;
-                return order;
-        }
-        // rank of each hit child among the hit children under the stable
-        // (dist, index) order: j < i precedes i  <=>  !(dist_i < dist_j)
-        uint32_t rk[8], fp[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-                rk[i] = 0;
-                fp[i] = 0;
-        }
-#pragma unroll
-        for (int i = 1; i < 8; ++i) {
-#pragma unroll
-                for (int j = 0; j < i; ++j) {
-                        const bool c = dist[i] < dist[j];  // i strictly first
-                        rk[j] += (uint32_t)(c & hit[i]);
-                        rk[i] += (uint32_t)(!c & hit[j]);
-                        if (kFullPos) {
-                                fp[j] += (uint32_t)c;
-                                fp[i] += (uint32_t)!c;
-                        }
-                }
-        }
-        uint32_t order = 0;
-        int n = 0;
-        full_pos = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-                order |= hit[i] ? ((uint32_t)i << (3 * rk[i])) : 0u;
-                n += hit[i] ? 1 : 0;
-                if (kFullPos)
-                        full_pos |= fp[i] << (3 * i);
-        }
-        cnt = n;
-        return order;
+        for (int i = 0; i < 8; ++i)
+                dist[i] = dist_of((uint32_t)i);
+        cnt = __popc(hm);
+        return rank_order8<kFullPos>(dist, hm, full_pos);
 }
 
-// v2 (fast path, uninstrumented): the same slab tests as v1, but the hit
-// children -- at most 4 for a line through 8 octants, save degenerate
-// boxes -- are ordered by a 4-slot sorting network on the total order
-// (dist, child index), which is exactly the stable order v1's ranks and
-// libstdc++'s insertion sort produce (strict <, ties by index; no dist is
-// NaN on the fast path).  A wave with any lane at > 4 hit children takes
-// v1's rank path.
-__device__ __forceinline__ void ce4(float &da, uint32_t &ia, float &db, uint32_t &ib)
-{
-        const bool sw = (db < da) | ((db == da) & (ib < ia));
-        const float td = da;
-        const uint32_t ti = ia;
-        da = sw ? db : da;
-        ia = sw ? ib : ia;
-        db = sw ? td : db;
-        ib = sw ? ti : ib;
-}
-
-__device__ __forceinline__ void ce4_lt(float &da, uint32_t &ia, float &db, uint32_t &ib)
-{
-        const bool sw = db < da;
-        const float td = da;
-        const uint32_t ti = ia;
-        da = sw ? db : da;
-        ia = sw ? ib : ia;
-        db = sw ? td : db;
-        ib = sw ? ti : ib;
-}
-
+// v2 (fast path, uninstrumented): the same slab tests as v1, the hit
+// children ordered by two_slot_order / net4_order when no lane of the wave
+// has more than 2 / 4 of them (rank_order8 otherwise); the travorder
+// distances are finished only when some lane orders >= 2 children.
 // kStd: every lane's ray has tmin == +0 and tmax == FLT_MAX, so (fast path,
 // no NaN) `t >= tmin && t <= tmax` is exactly "t is +-0, +subnormal or
 // +normal" -- one v_cmp_class instead of two compares and an AND.
-#ifndef VRT_TWO_SLOT
-#define VRT_TWO_SLOT 2  // 1: two-slot path when no lane has > 2 hit children; 2: also the <= 1 shortcut
-#endif
 template <bool kStd>
 __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float bmax[3], const RayK &r, int &cnt,
                                               uint32_t content)
@@ -280,19 +346,11 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
                 const int mx = (i >> 2) & 1, my = (i >> 1) & 1, mz = i & 1;
-#ifndef VRT_MAX3
-#define VRT_MAX3 1
-#endif
-#if VRT_MAX3
                 // one v_max3 / v_min3 per child: the compiler otherwise
                 // shares the pairwise max of two axes (24 ops instead of 16)
                 float t0, t1;
                 asm("v_max3_f32 %0, %1, %2, %3" : "=v"(t0) : "v"(nr[0][mx]), "v"(nr[1][my]), "v"(nr[2][mz]));
                 asm("v_min3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(fr[0][mx]), "v"(fr[1][my]), "v"(fr[2][mz]));
-#else
-                const float t0 = fmaxf(fmaxf(nr[0][mx], nr[1][my]), nr[2][mz]);
-                const float t1 = fminf(fminf(fr[0][mx], fr[1][my]), fr[2][mz]);
-#endif
                 bool in0, in1;
                 if (kStd) {
                         in0 = __builtin_amdgcn_classf(t0, 0x1E0);  // -0, +0, +subnormal, +normal
@@ -307,7 +365,7 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
         hm &= content;
         const int n = __popc(hm);
         cnt = n;
-        if (VRT_TWO_SLOT >= 2 && __all(n <= 1))
+        if (__all(n <= 1))
                 return (uint32_t)__builtin_ctz(hm | 0x100u) & 7u;  // one or no hit child: nothing to order
         // travorder distances dot(d, centre - o), finished only when some
         // lane orders >= 2 children (camera rays, kStd)
@@ -318,143 +376,22 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
                 q[k][1] = kStd ? dd[k] * (cm[k][1] - oo[k]) : cm[k][1];
         }
         const float qx0 = 0.0f + q[0][0], qx1 = 0.0f + q[0][1];
+        auto dist_of = [&](uint32_t ci) {
+                return (((ci & 4u) ? qx1 : qx0) + ((ci & 2u) ? q[1][1] : q[1][0])) +
+                       ((ci & 1u) ? q[2][1] : q[2][0]);
+        };
         if (__any(n > 4)) {
-                // rare: v1's full rank order over the same mask
+                // rare: the full rank order over the same mask
                 float dist[8];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                        const int mx = (i >> 2) & 1, my = (i >> 1) & 1, mz = i & 1;
-                        dist[i] = ((mx ? qx1 : qx0) + q[1][my]) + q[2][mz];
-                }
-                uint32_t rk[8];
-#pragma unroll
                 for (int i = 0; i < 8; ++i)
-                        rk[i] = 0;
-#pragma unroll
-                for (int i = 1; i < 8; ++i)
-#pragma unroll
-                        for (int j = 0; j < i; ++j) {
-                                const bool c = dist[i] < dist[j];
-                                rk[j] += (uint32_t)(c & ((hm >> i) & 1u));
-                                rk[i] += (uint32_t)(!c & ((hm >> j) & 1u));
-                        }
-                uint32_t order = 0;
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-                        order |= ((hm >> i) & 1u) ? ((uint32_t)i << (3 * rk[i])) : 0u;
-                return order;
+                        dist[i] = dist_of((uint32_t)i);
+                uint32_t fp_unused;
+                return rank_order8<false>(dist, hm, fp_unused);
         }
-        if (VRT_TWO_SLOT && __all(n <= 2)) {
-                // common case: no lane has more than 2 hit children -- two
-                // slots, one comparator (ties keep index order: i0 < i1)
-                const uint32_t i0 = (uint32_t)__builtin_ctz(hm | 0x100u);
-                const uint32_t m1 = hm & (hm - 1u);
-                const uint32_t i1 = (uint32_t)__builtin_ctz(m1 | 0x100u);
-                auto dist_of = [&](uint32_t ci) {
-                        return (((ci & 4u) ? qx1 : qx0) + ((ci & 2u) ? q[1][1] : q[1][0])) +
-                               ((ci & 1u) ? q[2][1] : q[2][0]);
-                };
-                const float d0 = dist_of(i0);
-                const float d1 = i1 < 8u ? dist_of(i1) : __int_as_float(0x7f800000);
-                const bool sw = d1 < d0;
-                return sw ? ((i1 & 7u) | ((i0 & 7u) << 3)) : ((i0 & 7u) | ((i1 & 7u) << 3));
-        }
-        // up to 4 hit children into slots in index order; empty slots sort last
-        float d[4];
-        uint32_t id[4];
-        uint32_t m = hm;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-                const uint32_t i = m ? (uint32_t)__builtin_ctz(m) : 8u;
-                m &= m - 1u;
-                const uint32_t mx = (i >> 2) & 1u, my = (i >> 1) & 1u, mz = i & 1u;
-                const float dv = ((mx ? qx1 : qx0) + (my ? q[1][1] : q[1][0])) + (mz ? q[2][1] : q[2][0]);
-                d[k] = i < 8u ? dv : __int_as_float(0x7f800000);
-                id[k] = i;
-        }
-        // The slots start in index order, so in the first two layers the
-        // element in the lower slot always has the lower index ((0,1),(2,3)
-        // trivially; (0,2),(1,3) compare a slot-{0,1} child with a
-        // slot-{2,3} one): ties keep the order and the comparison reduces
-        // to dist.  Only the last comparator (1,2) needs the index.
-        ce4_lt(d[0], id[0], d[1], id[1]);
-        ce4_lt(d[2], id[2], d[3], id[3]);
-        ce4_lt(d[0], id[0], d[2], id[2]);
-        ce4_lt(d[1], id[1], d[3], id[3]);
-        ce4(d[1], id[1], d[2], id[2]);
-        return (id[0] & 7u) | ((id[1] & 7u) << 3) | ((id[2] & 7u) << 6) | ((id[3] & 7u) << 9);
-}
-
-template <bool kFullPos>
-__device__ __forceinline__ uint32_t expand_v0(const float bmin[3],
-                                           const float bmax[3],
-                                           const RayK &r, int &cnt,
-                                           uint32_t &full_pos)
-{
-        const float oo[3] = { r.o.x, r.o.y, r.o.z };
-        const float dd[3] = { r.d.x, r.d.y, r.d.z };
-        const float di[3] = { r.dinv.x, r.dinv.y, r.dinv.z };
-        float nr[3][2], fr[3][2], q[3][2];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-                // split(): half = size()/2; child.min = min + mask*half;
-                // child.max = child.min + half
-                const float h = (bmax[k] - bmin[k]) / 2.0f;
-                const float a0 = bmin[k] + 0.0f * h;  // mask 0 min
-                const float b = bmin[k] + h;          // mask 0 max == mask 1 min
-                const float a1 = a0 + h;              // mask 0 max (same op as b)
-                const float c = b + h;                // mask 1 max
-                // AABB3D::isect: (min - o) * dinv, (max - o) * dinv
-                const float ta = (a0 - oo[k]) * di[k];
-                const float tb0 = (a1 - oo[k]) * di[k];
-                const float tb1 = (b - oo[k]) * di[k];
-                const float tc = (c - oo[k]) * di[k];
-                nr[k][0] = std_min(ta, tb0);
-                fr[k][0] = std_max(ta, tb0);
-                nr[k][1] = std_min(tb1, tc);
-                fr[k][1] = std_max(tb1, tc);
-                // travorder: dot(d, center - o), center = (min + max) * .5f
-                q[k][0] = dd[k] * ((a0 + a1) * .5f - oo[k]);
-                q[k][1] = dd[k] * ((b + c) * .5f - oo[k]);
-        }
-        float dist[8];
-        uint32_t hm = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-                const int mx = (i >> 2) & 1, my = (i >> 1) & 1, mz = i & 1;
-                float t0 = nr[0][mx], t1 = fr[0][mx];
-                if (t0 < nr[1][my]) t0 = nr[1][my];  // max_element
-                if (t0 < nr[2][mz]) t0 = nr[2][mz];
-                if (fr[1][my] < t1) t1 = fr[1][my];  // min_element
-                if (fr[2][mz] < t1) t1 = fr[2][mz];
-                hm |= (slab_hit(t0, t1, r.tmin, r.tmax) ? 1u : 0u) << i;
-                dist[i] = (0.0f + q[0][mx] + q[1][my]) + q[2][mz];
-        }
-        // Stable order: j precedes i  <=>  !(dist_i < dist_j) for j < i.
-        uint32_t bef[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-                bef[i] = 0;
-#pragma unroll
-        for (int i = 1; i < 8; ++i) {
-#pragma unroll
-                for (int j = 0; j < i; ++j) {
-                        const bool c = dist[i] < dist[j];
-                        bef[i] |= (c ? 0u : 1u) << j;
-                        bef[j] |= (c ? 1u : 0u) << i;
-                }
-        }
-        uint32_t order = 0;
-        full_pos = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-                const uint32_t pos = __popc(bef[i] & hm);
-                order |= ((hm >> i) & 1u) ? ((uint32_t)i << (3 * pos)) : 0u;
-                if (kFullPos)
-                        full_pos |= (uint32_t)__popc(bef[i]) << (3 * i);
-        }
-        cnt = __popc(hm);
-        return order;
+        if (__all(n <= 2))
+                return two_slot_order(dist_of, hm);  // common case
+        return net4_order(dist_of, hm);
 }
 
 template <bool kFullPos, bool kFast, bool kStd = false>
@@ -463,15 +400,9 @@ __device__ __forceinline__ uint32_t expand(const float bmin[3],
                                            const RayK &r, int &cnt,
                                            uint32_t &full_pos, uint32_t content)
 {
-#if VRT_EXPAND_V == 0
-        return expand_v0<kFullPos>(bmin, bmax, r, cnt, full_pos);
-#elif VRT_EXPAND_V == 2
         if (kFast && !kFullPos)
                 return expand_v2<kStd>(bmin, bmax, r, cnt, content);
         return expand_v1<kFullPos, kFast>(bmin, bmax, r, cnt, full_pos, content);
-#else
-        return expand_v1<kFullPos, kFast>(bmin, bmax, r, cnt, full_pos, content);
-#endif
 }
 
 struct MarchResult {
@@ -483,9 +414,15 @@ struct MarchResult {
         uint32_t A, L, T;  // reference-equivalent counters (instrumented)
 };
 
-#ifndef VRT_LEAF_V
-#define VRT_LEAF_V 2
-#endif
+// ray_march_isect's std::min_element over the records (VRT/voxel_octree.cc:
+// 122-125, `lhs.depth < rhs.depth`): a record replaces the best one only when
+// none is kept yet or its depth is strictly smaller, so the FIRST minimum in
+// leaf order wins (pinned against the real std::min_element by
+// k_selftest_order / tests/golden/travorder_std.cpp).
+__device__ __forceinline__ bool first_min_takes(bool any, float best, float depth)
+{
+        return !any || depth < best;
+}
 
 // ray_march_isect (VRT/voxel_octree.cc:99-129) over one leaf's records, with
 // intersect_triangle3 (VRT/raytri.cc:197-249) inlined in a register-frugal
@@ -578,7 +515,7 @@ __device__ __forceinline__ bool leaf_isect_v2(const void *__restrict__ refs,
                 const float tf = (float)t;
                 const f3 hp = r.o + r.d * tf;
                 const float depth = length(hp - r.o);
-                if (!any || depth < best) {  // min_element: first strict minimum
+                if (first_min_takes(any, best, depth)) {
                         any = true;
                         best = depth;
                         best_t = tf;
@@ -1195,45 +1132,36 @@ __global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k
 // b, b+8, ... share an XCD and its L2; an XCD's counter covers one
 // contiguous slice of the tiles) and moves on to the other XCDs' counters
 // when its own is exhausted.  One-wave workgroups top out at 16 resident
-// waves per CU (the per-CU workgroup limit); here 24 are resident and a
-// wave never waits for a workgroup sibling.  The last wave out resets the
-// counters for the next launch (stream order; a scene renders on one
-// stream at a time).
+// waves per CU (the per-CU workgroup limit); at VRT_PERSIST_WAVES_PER_EU = 5
+// this kernel keeps 5 waves per SIMD = 20 per CU resident, and a wave never
+// waits for a workgroup sibling.  The counters belong to this launch alone
+// (WorkQueue, vrt_internal.h): nothing is reset at the end.
 constexpr int kPersistBlock = 256;
 #ifndef VRT_PERSIST_WAVES_PER_EU
 #define VRT_PERSIST_WAVES_PER_EU 5
 #endif
-template <bool kR64>
 __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_render_p(RenderParams p)
 {
         __shared__ uint2 stk[kStack * kPersistBlock];
         const int tid = threadIdx.x, lane = tid & 63;
-        uint32_t *ctr = p.sc.ctr;
         const int units = p.tiles_this_rank * 4;
-        const int per = (units + 7) >> 3;
         const int xcd = blockIdx.x & 7;
         for (int j = 0; j < 8; ++j) {
                 const int x = (xcd + j) & 7;
-                const int lo = x * per, hi = min(units, lo + per);
+                int lo, hi;
+                queue_range(units, x, lo, hi);
                 if (lo >= hi)
                         continue;
                 for (;;) {
                         uint32_t u = 0;
                         if (lane == 0)
-                                u = atomicAdd(ctr + x * kCtrStride, 1u);
-                        u = __builtin_amdgcn_readfirstlane(u);
-                        const int unit = lo + (int)u;
-                        if (unit >= hi)
+                                u = atomicAdd(p.q.ctr + x * kQueueStride, 1u);
+                        u = __builtin_amdgcn_readfirstlane(u) - p.q.base[x];
+                        if (u >= (uint32_t)(hi - lo))
                                 break;
-                        render_unit<false, kR64, kPersistBlock>(p, unit >> 2, unit & 3, lane, stk + tid, nullptr,
-                                                                nullptr);
-                }
-        }
-        if (lane == 0) {
-                const uint32_t nw = gridDim.x * (kPersistBlock / 64);
-                if (atomicAdd(ctr + 8 * kCtrStride, 1u) == nw - 1u) {
-                        for (int x = 0; x <= 8; ++x)
-                                atomicExch(ctr + x * kCtrStride, 0u);
+                        const int unit = lo + (int)u;
+                        render_unit<false, false, kPersistBlock>(p, unit >> 2, unit & 3, lane, stk + tid, nullptr,
+                                                                 nullptr);
                 }
         }
 }
@@ -1544,43 +1472,113 @@ __global__ void k_selftest(const double *mt_in, double *mt_out,
         }
 }
 
-hipError_t launch_render(const RenderParams &p, bool instrumented,
-                         hipStream_t st)
+// The kernel's own travorder / min_element code on arbitrary inputs (the
+// std::sort / std::min_element pin, tests/golden/travorder_std.cpp).  Per
+// case i: dist[8i..8i+7], hit mask hm[i] ->
+//   out[6i+0] insertion_perm8 (the full order, 3-bit fields)
+//   out[6i+1] perm_filter of it | count << 24 (the exact path's result)
+//   out[6i+2] rank_order8 | popc(hm) << 24     (fast paths: no NaN)
+//   out[6i+3] two_slot_order                    (no NaN, <= 2 hit children)
+//   out[6i+4] net4_order                        (no NaN, <= 4 hit children)
+//   out[6i+5] rank_order8's full position word  (instrumented counters)
+// and per record list j: depth[j*stride .. + len[j]) -> argmin[j] (first
+// minimum by first_min_takes, -1 if empty).
+__global__ void k_selftest_order(const float *__restrict__ dist, const uint32_t *__restrict__ hm, int64_t n,
+                                 uint32_t *__restrict__ out, const float *__restrict__ depth,
+                                 const int32_t *__restrict__ len, int64_t m, int32_t stride,
+                                 int32_t *__restrict__ argmin)
 {
-        if (p.tiles_this_rank <= 0)
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i < n) {
+                float d[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                        d[k] = dist[8 * i + k];
+                const uint32_t mask = hm[i] & 0xFFu;
+                auto dist_of = [&](uint32_t ci) { return d[ci & 7u]; };
+                const uint32_t perm = insertion_perm8(dist_of);
+                int cnt = 0;
+                uint32_t fp = 0;
+                const uint32_t ex = perm_filter<false>(perm, mask, cnt, fp);
+                const uint32_t rk = rank_order8<true>(d, mask, fp);
+                out[6 * i + 0] = perm;
+                out[6 * i + 1] = ex | ((uint32_t)cnt << 24);
+                out[6 * i + 2] = rk | ((uint32_t)__popc(mask) << 24);
+                out[6 * i + 3] = two_slot_order(dist_of, mask);
+                out[6 * i + 4] = net4_order(dist_of, mask);
+                out[6 * i + 5] = fp;
+        }
+        if (i < m) {
+                bool any = false;
+                float best = 0.f;
+                int32_t bi = -1;
+                for (int32_t k = 0; k < len[i]; ++k) {
+                        const float v = depth[i * stride + k];
+                        if (first_min_takes(any, best, v)) {
+                                any = true;
+                                best = v;
+                                bi = k;
+                        }
+                }
+                argmin[i] = bi;
+        }
+}
+
+hipError_t launch_selftest_order(const float *dist, const uint32_t *hm, int64_t n, uint32_t *out,
+                                 const float *depth, const int32_t *len, int64_t m, int32_t stride,
+                                 int32_t *argmin, hipStream_t st)
+{
+        const int64_t nt = std::max(n, m);
+        if (nt <= 0)
                 return hipSuccess;
-        // round the grid up to a multiple of 8 (one slot per XCD)
-        const int grid = (p.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
-        const bool w = p.sc.wide_leaves != 0;
+        hipLaunchKernelGGL(k_selftest_order, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, dist, hm, n,
+                           out, depth, len, m, stride, argmin);
+        return hipGetLastError();
+}
+
 #ifndef VRT_PERSIST
 #define VRT_PERSIST 1
 #endif
-        // persistent waves for RefRec48 scenes; large-leaf (RefRec64) scenes
-        // keep one-wave workgroups (-11 % persistent at depth 6)
-        if (VRT_PERSIST && !instrumented && !w && p.sc.ctr) {
+// persistent waves for RefRec48 scenes; large-leaf (RefRec64) scenes keep
+// one-wave workgroups (-11 % persistent at depth 6)
+bool render_uses_queue(const DevScene &sc, bool instrumented)
+{
+        return VRT_PERSIST && !instrumented && !sc.wide_leaves && sc.persist_blocks > 0;
+}
+
+hipError_t persistent_render_blocks(int *blocks)
+{
+        int per_cu = 0, dev = 0;
+        hipDeviceProp_t prop;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess)
+                e = hipGetDeviceProperties(&prop, dev);
+        if (e == hipSuccess)
+                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_render_p, kPersistBlock, 0);
+        if (e != hipSuccess)
+                return e;
+        *blocks = std::max(8, (per_cu * prop.multiProcessorCount) & ~7);
+        return hipSuccess;
+}
+
+hipError_t launch_render(const RenderParams &p, bool instrumented,
+                         hipStream_t st, int *queue_waves)
+{
+        *queue_waves = 0;
+        if (p.tiles_this_rank <= 0)
+                return hipSuccess;
+        const bool w = p.sc.wide_leaves != 0;
+        if (render_uses_queue(p.sc, instrumented)) {
                 // one resident generation of 4-wave workgroups (<= one per
                 // 4 units, a multiple of 8 for the XCD map)
-                static int blocks[2] = { 0, 0 };
-                int &nb = blocks[w ? 1 : 0];
-                if (nb == 0) {
-                        void (*kp)(RenderParams) = w ? k_render_p<true> : k_render_p<false>;
-                        int per_cu = 0, dev = 0;
-                        hipDeviceProp_t prop;
-                        hipError_t e = hipGetDevice(&dev);
-                        if (e == hipSuccess)
-                                e = hipGetDeviceProperties(&prop, dev);
-                        if (e == hipSuccess)
-                                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kPersistBlock, 0);
-                        if (e != hipSuccess)
-                                return e;
-                        nb = std::max(8, (per_cu * prop.multiProcessorCount) & ~7);
-                }
                 const int need = (p.tiles_this_rank + 7) & ~7;  // 4 units per tile, 4 waves per block
-                const int g = std::min(nb, need);
-                hipLaunchKernelGGL(w ? k_render_p<true> : k_render_p<false>, dim3(g), dim3(kPersistBlock), 0, st,
-                                   p);
+                const int g = std::min(p.sc.persist_blocks, need);
+                hipLaunchKernelGGL(k_render_p, dim3(g), dim3(kPersistBlock), 0, st, p);
+                *queue_waves = g * (kPersistBlock / 64);
                 return hipGetLastError();
         }
+        // round the grid up to a multiple of 8 (one slot per XCD)
+        const int grid = (p.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
         void (*kern)(RenderParams) = instrumented ? (w ? k_render<true, true> : k_render<true, false>)
                                                   : (w ? k_render<false, true> : k_render<false, false>);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kRenderBlock), 0, st, p);
