@@ -25,8 +25,12 @@ all: $(PKG)/libvrt.so oracle
 $(BLD):
 	mkdir -p $(BLD)
 
+# wave-level atomic aggregation by a DPP scan (the default iterative scan
+# loops over the active lanes; take_unit() adds a lane-varying value)
+KFLAGS := -mllvm -amdgpu-atomic-optimizer-strategy=DPP
+
 $(BLD)/vrt_kernels.o: $(SRC)/vrt_kernels.hip $(HDRS) | $(BLD)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -c $< -o $@
 
 $(BLD)/vrt_sort.o: $(SRC)/vrt_sort.hip $(HDRS) | $(BLD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -68,14 +72,14 @@ oracle:
 # A/B variant of the kernels:  make variant NAME=v0 DEFS="-DVRT_EXPAND_V=0"
 variant: $(HOSTOBJS) $(BLD)/vrt_sort.o $(BLD)/vrt_build.o | $(BLD)
 	mkdir -p build/variants
-	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
 	  build/variants/k_$(NAME).o $(BLD)/vrt_sort.o $(BLD)/vrt_build.o $(HOSTOBJS) -lpthread
 
 # variant that also rebuilds the host side (for data-layout changes)
 fullvariant: $(BLD)/vrt_sort.o $(BLD)/vrt_build.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o | $(BLD)
 	mkdir -p build/variants
-	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_host.cpp -o build/variants/h_$(NAME).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
 	  build/variants/k_$(NAME).o build/variants/h_$(NAME).o $(BLD)/vrt_sort.o $(BLD)/vrt_build.o \
@@ -83,7 +87,7 @@ fullvariant: $(BLD)/vrt_sort.o $(BLD)/vrt_build.o $(BLD)/vrt_hdr.o $(BLD)/vrt_pr
 
 # ISA listing + register/occupancy report of the kernels (for DESIGN.md)
 isa: | $(BLD)
-	$(HIPCC) $(HIPFLAGS) --offload-device-only -S $(SRC)/vrt_kernels.hip -o $(BLD)/vrt_kernels.s \
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) --offload-device-only -S $(SRC)/vrt_kernels.hip -o $(BLD)/vrt_kernels.s \
 	  -Rpass-analysis=kernel-resource-usage 2> $(BLD)/resource_usage.txt || true
 
 clean:

@@ -218,6 +218,13 @@ int vrt_ray_march_batch_device(vrt_scene *s, const vrt_ray *d_rays, int64_t n,
 int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
                         const float *sat_in, int32_t *sat_out, int64_t n);
 
+/* Test hook: process-wide flags read by every later render launch.
+ * VRT_TEST_FORCE_DEFER makes the persistent fast-path kernel defer every
+ * unit to its exact fallback pass (k_render_defer), so tests can pin that
+ * rarely taken path against the oracle.  0 = normal operation. */
+#define VRT_TEST_FORCE_DEFER 1
+int vrt_set_test_flags(int flags);
+
 /* The kernels' own travorder sort (std::sort of the 8 Items by dist,
  * VRT/voxel_octree.cc:77-97) and ray_march_isect min_element
  * (VRT/voxel_octree.cc:122-125) on arbitrary inputs, for the pin against

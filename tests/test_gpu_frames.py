@@ -157,6 +157,32 @@ def test_two_streams_share_one_scene(proxy):
     assert np.array_equal(bits(a), bits(want[0]))
 
 
+def test_forced_defer_pass_matches_oracle(proxy):
+    """The persistent fast-path kernel defers a unit whose rays need the
+    exact march (a non-zero denormal direction component); k_render_defer
+    renders the deferred units afterwards.  With every unit forced onto that
+    path (VRT_TEST_FORCE_DEFER) the images still equal the oracle's: a small
+    film (deferred list within its capacity) and a 1080p film (32,400 units:
+    more than the list holds, so the fallback re-renders every unit)."""
+    tree, osc = scenes(proxy, 8)
+    mn, mx = tree.root_box
+    try:
+        vrt.set_test_flags(vrt.TEST_FORCE_DEFER)
+        for (nx, ny, pose) in ((64, 48, 2), (1920, 1080, 11)):
+            p = vrt.sweep_pose(mn, mx, pose, 16)
+            want = osc.render(po.camera(*p), 1.0, 1.0, nx, ny, nthreads=NTH, samples=False)
+            got = _device_image(tree, vrt.Camera(*p), vrt.Film(1, 1, nx, ny))
+            assert np.array_equal(bits(got), bits(want)), (nx, ny)
+    finally:
+        vrt.set_test_flags(0)
+    # the count was reset: a normal launch of the same slot ring renders fully
+    p = vrt.sweep_pose(mn, mx, 3, 16)
+    want = osc.render(po.camera(*p), 1.0, 1.0, 320, 200, nthreads=NTH, samples=False)
+    for _ in range(10):  # cycles the 8-slot ring
+        got = _device_image(tree, vrt.Camera(*p), vrt.Film(1, 1, 320, 200))
+        assert np.array_equal(bits(got), bits(want))
+
+
 def _pack(seq):
     w = 0
     for k, c in enumerate(seq):

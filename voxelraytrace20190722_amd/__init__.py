@@ -10,7 +10,7 @@ from .api import (  # noqa: F401
     FLT_MAX, Camera, Film, ObjModel, SceneData, VoxelOctree, build_id, device_count, device_selftest,
     device_selftest_order,
     hdr_bytes, hdr_bytes_from_rgbe, intersect_triangle3, load_image, make_ray, obj2voxel, ray_march, ray_march_init,
-    render, sweep_pose, tga_decode, tiles_per_rank, to_radian, tri_box_overlap,
+    TEST_FORCE_DEFER, render, set_test_flags, sweep_pose, tga_decode, tiles_per_rank, to_radian, tri_box_overlap,
     unpack_tiles_device, write_hdr, rgbe_device, write_hdr_device,
 )
 
@@ -19,5 +19,5 @@ __all__ = [
     "device_count", "device_selftest", "hdr_bytes", "intersect_triangle3", "make_ray",
     "ray_march", "ray_march_init", "render", "sweep_pose", "tiles_per_rank", "to_radian",
     "tri_box_overlap", "unpack_tiles_device", "write_hdr", "ObjModel", "obj2voxel", "load_image",
-    "tga_decode", "hdr_bytes_from_rgbe", "rgbe_device", "write_hdr_device", "build_id", "device_selftest_order",
+    "tga_decode", "hdr_bytes_from_rgbe", "rgbe_device", "write_hdr_device", "build_id", "device_selftest_order", "set_test_flags",
 ]

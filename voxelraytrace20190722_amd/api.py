@@ -576,6 +576,14 @@ def build_id():
     return lib().vrt_build_id().decode()
 
 
+TEST_FORCE_DEFER = 1  # include/vrt.h VRT_TEST_FORCE_DEFER
+
+
+def set_test_flags(flags):
+    """Test hook (vrt_set_test_flags): flags read by every later launch."""
+    check(lib().vrt_set_test_flags(int(flags)), "vrt_set_test_flags")
+
+
 def device_count():
     n = C.c_int32()
     check(lib().vrt_device_count(C.byref(n)), "vrt_device_count")

@@ -677,7 +677,8 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         s->dev.texs = reinterpret_cast<const TexRec *>(base + off[6]);
         s->dev.tex_data = reinterpret_cast<const uint8_t *>(base + off[7]);
         s->d_queue = reinterpret_cast<uint32_t *>(base + off[8]);
-        HIPCHK(persistent_render_blocks(&s->dev.persist_blocks));
+        HIPCHK(persistent_blocks(&s->dev.persist_blocks, &s->dev.sec_blocks));
+        s->dev.nnodes = (int32_t)s->nodes.size();
         s->dev.max_depth = s->max_depth;
         s->dev.nmat = (int32_t)s->mats.size();
         s->dev.ntex = (int32_t)s->texs.size();
@@ -919,6 +920,14 @@ extern "C" int vrt_tiles_per_rank(const vrt_film *film, int nranks)
         return (T + nranks - 1) / nranks;
 }
 
+static std::atomic<int> g_test_flags{0};
+
+extern "C" int vrt_set_test_flags(int flags)
+{
+        g_test_flags.store(flags);
+        return VRT_OK;
+}
+
 static void fill_render_params(vrt_scene *s, const vrt_camera *cam,
                                const vrt_film *film, int rank, int nranks,
                                RenderParams *p)
@@ -932,37 +941,71 @@ static void fill_render_params(vrt_scene *s, const vrt_camera *cam,
         p->nranks = nranks;
         const int T = p->ntx * p->nty;
         p->tiles_this_rank = rank < T ? (T - rank + nranks - 1) / nranks : 0;
+        p->test_flags = g_test_flags.load();
 }
 
-// One render launch on stream st (caller holds s->mu).  A persistent launch
-// takes the next work-queue slot of the scene's ring: st first waits for the
+static float scene_res(const vrt_scene *s);
+
+// Work-queue ring (WorkQueue, vrt_internal.h; caller holds s->mu).  A
+// persistent launch takes the next slot: its stream first waits for the
 // slot's previous launch (on whatever stream it ran), the kernel takes its
 // units from base[] on, and the slot's bases advance by exactly the adds the
-// launch makes (WorkQueue, vrt_internal.h).
+// launch makes.
+static int queue_take(vrt_scene *s, hipStream_t st, WorkQueue *q, int *slot)
+{
+        *slot = s->q_next;
+        s->q_next = (*slot + 1) % kQueueSlots;
+        if (s->q_live[*slot])
+                HIPCHK(hipStreamWaitEvent(st, s->q_ev[*slot], 0));
+        q->ctr = s->d_queue + (size_t)*slot * kQueueWords;
+        q->defer = q->ctr + 8 * kQueueStride;
+        std::memcpy(q->base, s->q_base[*slot], sizeof q->base);
+        return VRT_OK;
+}
+
+static int queue_release(vrt_scene *s, int slot, hipStream_t st, int units, int waves)
+{
+        for (int x = 0; x < 8; ++x) {
+                int lo, hi;
+                queue_range(units, x, lo, hi);
+                if (hi > lo)
+                        s->q_base[slot][x] += (uint32_t)(hi - lo) + (uint32_t)waves;
+        }
+        HIPCHK(hipEventRecord(s->q_ev[slot], st));
+        s->q_live[slot] = true;
+        return VRT_OK;
+}
+
+// One render launch on stream st (caller holds s->mu).
 static int render_launch(vrt_scene *s, RenderParams &p, bool instrumented, hipStream_t st)
 {
         int slot = -1;
-        if (render_uses_queue(p.sc, instrumented)) {
-                slot = s->q_next;
-                s->q_next = (slot + 1) % kQueueSlots;
-                if (s->q_live[slot])
-                        HIPCHK(hipStreamWaitEvent(st, s->q_ev[slot], 0));
-                p.q.ctr = s->d_queue + (size_t)slot * (kQueueBytes / sizeof(uint32_t));
-                std::memcpy(p.q.base, s->q_base[slot], sizeof p.q.base);
-        }
-        int waves = 0;
-        HIPCHK(launch_render(p, instrumented, st, &waves));
-        if (slot >= 0 && waves > 0) {
-                const int units = p.tiles_this_rank * 4;
-                for (int x = 0; x < 8; ++x) {
-                        int lo, hi;
-                        queue_range(units, x, lo, hi);
-                        if (hi > lo)
-                                s->q_base[slot][x] += (uint32_t)(hi - lo) + (uint32_t)waves;
-                }
-                HIPCHK(hipEventRecord(s->q_ev[slot], st));
-                s->q_live[slot] = true;
-        }
+        if (render_kind(p, instrumented) != kRenderGrid)
+                if (int rc = queue_take(s, st, &p.q, &slot))
+                        return rc;
+        int waves = 0, units = 0;
+        HIPCHK(launch_render(p, instrumented, st, &waves, &units));
+        if (slot >= 0)
+                return queue_release(s, slot, st, units, waves);
+        return VRT_OK;
+}
+
+// One config-5 launch (k_primary1 + secondary rays) on stream st (caller
+// holds s->mu).
+static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int rank, int nranks, float *d_prim,
+                            float *d_vis, int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox, hipStream_t st)
+{
+        int slot = -1;
+        WorkQueue q;
+        std::memset(&q, 0, sizeof q);
+        if (secondary_uses_queue(p.sc))
+                if (int rc = queue_take(s, st, &q, &slot))
+                        return rc;
+        int waves = 0, units = 0;
+        HIPCHK(launch_secondary(p, spp, rank, nranks, scene_res(s), d_prim, d_vis, s_hit, s_tri, s_vox,
+                                slot >= 0 ? &q : nullptr, st, &waves, &units));
+        if (slot >= 0)
+                return queue_release(s, slot, st, units, waves);
         return VRT_OK;
 }
 
@@ -1181,8 +1224,8 @@ extern "C" int vrt_render_secondary_device(vrt_scene *s, const vrt_camera *cam,
         fill_render_params(s, cam, film, 0, 1, &p);
         hipStream_t st = static_cast<hipStream_t>(stream);
         HIPCHK(hipEventRecord(s->ev0, st));
-        HIPCHK(launch_secondary(p, spp, rank, nranks, scene_res(s), d_prim, d_vis, nullptr, nullptr,
-                                nullptr, st));
+        if (int rc = secondary_launch(s, p, spp, rank, nranks, d_prim, d_vis, nullptr, nullptr, nullptr, st))
+                return rc;
         HIPCHK(hipEventRecord(s->ev1, st));
         s->timed = true;
         return VRT_OK;
@@ -1223,9 +1266,10 @@ extern "C" int vrt_render_secondary(vrt_scene *s, const vrt_camera *cam,
         RenderParams p;
         fill_render_params(s, cam, film, 0, 1, &p);
         HIPCHK(hipEventRecord(s->ev0, s->stream));
-        HIPCHK(launch_secondary(p, spp, 0, 1, scene_res(s), static_cast<float *>(dprim.p),
-                                static_cast<float *>(dvis.p), static_cast<int32_t *>(dh.p),
-                                static_cast<int32_t *>(dt.p), static_cast<uint32_t *>(dv.p), s->stream));
+        if (int rc = secondary_launch(s, p, spp, 0, 1, static_cast<float *>(dprim.p), static_cast<float *>(dvis.p),
+                                      static_cast<int32_t *>(dh.p), static_cast<int32_t *>(dt.p),
+                                      static_cast<uint32_t *>(dv.p), s->stream))
+                return rc;
         HIPCHK(hipEventRecord(s->ev1, s->stream));
         s->timed = true;
         HIPCHK(hipStreamSynchronize(s->stream));

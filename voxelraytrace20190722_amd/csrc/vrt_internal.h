@@ -90,23 +90,32 @@ struct DevScene {
                               // wave-uniform leaf loads (leaf_isect)
         int32_t persist_blocks;  // resident 256-thread blocks of the persistent render on this
                                  // device (a multiple of 8), 0 = no persistent launches
+        int32_t sec_blocks;      // the same for the persistent secondary-ray kernel
+        int32_t nnodes;          // node count (LDS node staging reads at most this many)
 };
 
-// Work queue of one persistent launch (k_render_p): 8 counters, one per XCD
-// slice of the units, one 128-B line each.  The kernel never resets them:
-// unit j of slice x is taken by the atomicAdd that returns base[x] + j, and
-// every wave makes exactly one more (failing) add per non-empty slice, so
-// after a launch of `waves` waves counter x has advanced by
-// (hi - lo of queue_range(units, x)) + waves -- the host keeps base[] from that, per ring
-// slot (vrt_host.cpp: take_queue / release_queue).  Launches on different
-// streams use different slots; a slot is reused only after its previous
-// launch has finished (an event), so no two launches share counters and no
-// memset is needed.
+// Work queue of one persistent launch (k_render_p, k_secondary_p): 8
+// counters, one per XCD slice of the units, one 128-B line each.  The
+// kernel never resets them: unit j of slice x is taken by the atomicAdd that
+// returns base[x] + j, and every wave makes exactly one more (failing) add
+// per non-empty slice, so after a launch of `waves` waves counter x has
+// advanced by (hi - lo of queue_range(units, x)) + waves -- the host keeps
+// base[] from that, per ring slot (vrt_host.cpp: queue_take /
+// queue_release).  Launches on different streams use different slots; a
+// slot is reused only after its previous launch has finished (an event), so
+// no two launches share counters and no memset is needed.
+// After the counters: the deferred-unit list of k_render_p<true> (count in
+// defer[0], units from defer[kDeferList]); k_render_defer, launched behind
+// it on the same stream, renders them and zeroes the count.
 constexpr int kQueueStride = 32;
 constexpr int kQueueSlots = 8;
-constexpr size_t kQueueBytes = 8 * kQueueStride * sizeof(uint32_t);
+constexpr int kDeferList = 32;
+constexpr int kDeferCap = 4096;
+constexpr size_t kQueueWords = 8 * kQueueStride + kDeferList + kDeferCap;
+constexpr size_t kQueueBytes = kQueueWords * sizeof(uint32_t);
 struct WorkQueue {
         uint32_t *ctr;
+        uint32_t *defer;
         uint32_t base[8];
 };
 // units of slice x: a contiguous range [lo, hi) of the unit order
@@ -144,6 +153,7 @@ struct RenderParams {
         int32_t rank, nranks;  // tile t handled by rank t % nranks
         int32_t tiles_this_rank;
         int32_t image_layout;  // 1: out is nx*ny*3 image; 0: packed tiles
+        int32_t test_flags;    // vrt_set_test_flags (VRT_TEST_FORCE_DEFER)
         float *out;
         SampleOut so;
         WorkQueue q;           // persistent launches only
@@ -205,22 +215,33 @@ hipError_t build_tree_device(int device, const float *pos, int ntri, const float
                              const float root_mx[3], int max_depth, DeviceBuild *out, std::string *err);
 
 // Kernel launchers (vrt_kernels.hip)
-// true when launch_render runs the persistent kernel, which takes its units
-// from p.q; *queue_waves = the waves launched (for the queue bases)
-bool render_uses_queue(const DevScene &sc, bool instrumented);
+// Which primary-render kernel launch_render runs: the one-wave grid
+// (k_render: instrumented, per-sample outputs, large-leaf scenes), the
+// persistent kernel (k_render_p<false>) or the persistent fast-only kernel
+// + its deferred-unit pass (k_render_p<true> + k_render_defer).  The
+// persistent kinds take their units from p.q.
+enum RenderKind { kRenderGrid = 0, kRenderPersist = 1, kRenderPersistFast = 2 };
+RenderKind render_kind(const RenderParams &p, bool instrumented);
+// *q_waves / *q_units = the failing adds each slice counter receives (the
+// waves launched that visit it) and the units queued (0 when no work queue
+// was used), for the queue bases
 hipError_t launch_render(const RenderParams &p, bool instrumented,
-                         hipStream_t st, int *queue_waves);
-// resident blocks of the persistent render on the current device
-hipError_t persistent_render_blocks(int *blocks);
+                         hipStream_t st, int *q_waves, int *q_units);
+// resident blocks of the persistent render / secondary kernels on the
+// current device
+hipError_t persistent_blocks(int *render_blocks, int *sec_blocks);
+bool secondary_uses_queue(const DevScene &sc);
 hipError_t launch_ray_march(const DevScene &sc, const void *d_rays,
                             int64_t n, void *d_hits, hipStream_t st);
 hipError_t launch_unpack(int nx, int ny, int ntx, int nty, int nranks,
                          int tiles_per_rank, const float *src, float *dst,
                          hipStream_t st);
+// q: the launch's work queue (persistent kernel) or nullptr (one wave per
+// pixel)
 hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,
                             int nranks, float res, float *prim, float *vis,
                             int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox,
-                            hipStream_t st);
+                            const WorkQueue *q, hipStream_t st, int *q_waves, int *q_units);
 hipError_t launch_light(const LightParams &p, hipStream_t st);
 // samp: n x 6 floats followed by room for their sorted copy (n x 6);
 // seg_start: max_seg entries (>= non-empty leaves), nseg zeroed

@@ -20,14 +20,23 @@
 //  * the DFS stack lives in LDS, [level][lane], 8 B per entry.
 //
 // VRT/x = /root/reference/VoxelRayTrace20190722/x
+#include "vrt.h"
 #include "vrt_internal.h"
 
+#include <algorithm>
 #include <climits>
+#include <cmath>
+#include <cstring>
 
 namespace vrt {
 
 constexpr int kBlock = 256;
-constexpr int kStack = 12;  // >= VRT_MAX_DEPTH - 1 internal levels
+// DFS stack entries per lane.  ray_march pushes only when it descends into
+// an internal child with siblings left, while walking the children of a
+// node at depth d <= max_depth - 2 (internal nodes end at depth
+// max_depth - 1), so at most max_depth - 2 entries are live.
+constexpr int kStack = 10;
+static_assert(kStack >= VRT_MAX_DEPTH - 1, "DFS stack too small for VRT_MAX_DEPTH");
 
 struct RayK {
         f3 o, d, dinv;
@@ -46,6 +55,46 @@ __device__ __forceinline__ void load_node(const NodeRec *__restrict__ nodes,
         bmax[0] = q0.w; bmax[1] = q1.x; bmax[2] = q1.y;
         a = __float_as_uint(q1.z);
         b = __float_as_uint(q1.w);
+}
+
+// LDS copy of the first kNS node records (the top BFS levels: node 0 is the
+// root, then whole levels in order), staged once per workgroup by
+// stage_nodes(); node i < kNS is read from it, the rest from HBM/L2.
+template <int kNS>
+__device__ __forceinline__ float4 *lds_node_table()
+{
+        __shared__ float4 t[kNS > 0 ? 2 * kNS : 1];
+        return t;
+}
+
+template <int kNS>
+__device__ __forceinline__ void stage_nodes(const NodeRec *__restrict__ nodes, int nnodes)
+{
+        if (kNS > 0) {
+                float4 *t = lds_node_table<kNS>();
+                const float4 *g = reinterpret_cast<const float4 *>(nodes);
+                const int n = 2 * (nnodes < kNS ? nnodes : kNS);
+                for (int i = threadIdx.x; i < n; i += blockDim.x)
+                        t[i] = g[i];
+                __syncthreads();
+        }
+}
+
+template <int kNS>
+__device__ __forceinline__ void load_node_st(const NodeRec *__restrict__ nodes, uint32_t i, float bmin[3],
+                                             float bmax[3], uint32_t &a, uint32_t &b)
+{
+        if (kNS > 0 && i < (uint32_t)kNS) {
+                const float4 *q = lds_node_table<kNS>() + 2 * i;
+                const float4 q0 = q[0];
+                const float4 q1 = q[1];
+                bmin[0] = q0.x; bmin[1] = q0.y; bmin[2] = q0.z;
+                bmax[0] = q0.w; bmax[1] = q1.x; bmax[2] = q1.y;
+                a = __float_as_uint(q1.z);
+                b = __float_as_uint(q1.w);
+        } else {
+                load_node(nodes, i, bmin, bmax, a, b);
+        }
 }
 
 // ---------------------------------------------------------------------------
@@ -555,7 +604,7 @@ __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, u
 
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).
-template <bool kCount, bool kFast, int kS, bool kStd, bool kUni, bool kR64>
+template <bool kCount, bool kFast, int kS, bool kStd, bool kUni, bool kR64, int kNS = 0>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint2 *stk,
                                           uint32_t *stk_aux,
@@ -568,7 +617,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         m.T = 0;
         float bmin[3], bmax[3];
         uint32_t a, b;
-        load_node(sc.nodes, 0, bmin, bmax, a, b);
+        load_node_st<kNS>(sc.nodes, 0, bmin, bmax, a, b);
         if (!aabb_isect(bmin, bmax, r.o, r.dinv, r.tmin, r.tmax))
                 return;
         if (a & kLeafBit) {
@@ -620,7 +669,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         node = base + ci;
                         if (kCount)
                                 path_rem[depth * kS] = 7u - ((fpos >> (3 * ci)) & 7u);
-                        load_node(sc.nodes, node, bmin, bmax, a, b);
+                        load_node_st<kNS>(sc.nodes, node, bmin, bmax, a, b);
                         if (!(a & kLeafBit)) {
                                 if (cnt) {
                                         stk[sp * kS] = make_uint2(base, order | ((uint32_t)cnt << 24));
@@ -674,7 +723,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 const uint32_t node = base + ci;
                 if (kCount)
                         path_rem[depth * kS] = 7u - ((fpos >> (3 * ci)) & 7u);
-                load_node(sc.nodes, node, bmin, bmax, a, b);
+                load_node_st<kNS>(sc.nodes, node, bmin, bmax, a, b);
                 if (!(a & kLeafBit)) {
                         if (cnt) {
                                 stk[sp * kS] = make_uint2(base, order | ((uint32_t)cnt << 24));
@@ -736,7 +785,7 @@ __device__ __forceinline__ bool fast_ok(const RayK &r)
         return ok;
 }
 
-template <bool kCount, int kS, bool kUni, bool kR64>
+template <bool kCount, int kS, bool kUni, bool kR64, int kNS = 0>
 __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const RayK &r,
                                                    uint2 *sb, uint32_t *sa, uint32_t *pr,
                                                    MarchResult &m)
@@ -746,11 +795,18 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
 #endif
         if (__all(sc.fast_ok && fast_ok(r))) {
                 if (VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
-                        ray_march<kCount, true, kS, true, kUni, kR64>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, true, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
                 else
-                        ray_march<kCount, true, kS, false, kUni, kR64>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, false, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
         } else
-                ray_march<kCount, false, kS, false, kUni, kR64>(sc, r, sb, sa, pr, m);
+                ray_march<kCount, false, kS, false, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
+}
+
+// True when ray_march's fast, standard-range instantiation is exact for
+// every lane of the wave (the first branch of ray_march_dispatch).
+__device__ __forceinline__ bool wave_fast_std(const DevScene &sc, const RayK &r)
+{
+        return __all(sc.fast_ok && fast_ok(r) && __float_as_uint(r.tmin) == 0u && r.tmax == kFltMax);
 }
 
 // ---------------------------------------------------------------------------
@@ -1023,8 +1079,13 @@ constexpr int kRenderBlock = 64 * VRT_RENDER_WAVES;
 // One work unit of the primary render: the 4x4-pixel quadrant `wave` of
 // this rank's k-th 8x8 tile, 4 gen_rays4 samples per pixel, one ray per
 // lane (lane = 4*pixel + sample).  stk_* are this lane's LDS stack columns.
-template <bool kCount, bool kR64, int kS>
-__device__ __forceinline__ void render_unit(const RenderParams &p, int k, int wave, int lane, uint2 *stk,
+// kSamples: the per-sample outputs p.so may be set (k_render); the
+// persistent kernels never write them.  kFastOnly: only ray_march's fast,
+// standard-range instantiation is compiled in (fewer live registers); a wave
+// whose rays need another path returns false before writing anything and the
+// caller defers the unit to k_render_defer.
+template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kNS = 0>
+__device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wave, int lane, uint2 *stk,
                                             uint32_t *stk_aux, uint32_t *path_rem)
 {
         const int t = p.rank + k * p.nranks;
@@ -1042,7 +1103,13 @@ __device__ __forceinline__ void render_unit(const RenderParams &p, int k, int wa
                                  dn, c.tmin, c.tmax);
 
         MarchResult m;
-        ray_march_dispatch<kCount, kS, true, kR64>(p.sc, r, stk, stk_aux, path_rem, m);
+        if (kFastOnly) {
+                if (!wave_fast_std(p.sc, r) || (p.test_flags & VRT_TEST_FORCE_DEFER))
+                        return false;
+                ray_march<false, true, kS, true, true, kR64, kNS>(p.sc, r, stk, nullptr, nullptr, m);
+        } else {
+                ray_march_dispatch<kCount, kS, true, kR64, kNS>(p.sc, r, stk, stk_aux, path_rem, m);
+        }
 
         f3 col;
         if (m.hit) {
@@ -1053,13 +1120,15 @@ __device__ __forceinline__ void render_unit(const RenderParams &p, int k, int wa
         }
 
         const size_t si = ((size_t)py * c.nx + px) * 4 + s;
-        if (p.so.hit) p.so.hit[si] = m.hit ? 1 : 0;
-        if (p.so.tri) p.so.tri[si] = m.hit ? (int32_t)m.tri : -1;
-        if (p.so.vox) p.so.vox[si] = m.hit ? p.sc.node_vox[m.node] : 0xFFFFFFFFu;
-        if (p.so.rgb) {
-                p.so.rgb[3 * si + 0] = col.x;
-                p.so.rgb[3 * si + 1] = col.y;
-                p.so.rgb[3 * si + 2] = col.z;
+        if (kSamples) {
+                if (p.so.hit) p.so.hit[si] = m.hit ? 1 : 0;
+                if (p.so.tri) p.so.tri[si] = m.hit ? (int32_t)m.tri : -1;
+                if (p.so.vox) p.so.vox[si] = m.hit ? p.sc.node_vox[m.node] : 0xFFFFFFFFu;
+                if (p.so.rgb) {
+                        p.so.rgb[3 * si + 0] = col.x;
+                        p.so.rgb[3 * si + 1] = col.y;
+                        p.so.rgb[3 * si + 2] = col.z;
+                }
         }
         if (kCount && p.so.cnt) {
                 p.so.cnt[4 * si + 0] = m.A;
@@ -1090,6 +1159,7 @@ __device__ __forceinline__ void render_unit(const RenderParams &p, int k, int wa
                 o[1] = acc[1];
                 o[2] = acc[2];
         }
+        return true;
 }
 
 template <bool kCount, bool kR64>
@@ -1127,43 +1197,94 @@ __global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k
                                       path_rem + (kCount ? tid : 0));
 }
 
-// Persistent variant (uninstrumented): 4-wave workgroups sized to fill the
-// chip once; every wave pulls quadrant units from a per-XCD counter (blocks
-// b, b+8, ... share an XCD and its L2; an XCD's counter covers one
-// contiguous slice of the tiles) and moves on to the other XCDs' counters
-// when its own is exhausted.  One-wave workgroups top out at 16 resident
-// waves per CU (the per-CU workgroup limit); at VRT_PERSIST_WAVES_PER_EU = 5
-// this kernel keeps 5 waves per SIMD = 20 per CU resident, and a wave never
-// waits for a workgroup sibling.  The counters belong to this launch alone
-// (WorkQueue, vrt_internal.h): nothing is reset at the end.
+// One dequeue from a WorkQueue counter for the whole wave: every lane takes
+// part in the add (lane 0 adds 1, the others 0; the compiler folds that into
+// one atomic) and the wave reads lane 0's result.  No lane-0-only branch
+// around the atomic: inside k_secondary_p's persistent loop that divergent
+// region was structurized into a loop that re-ran one pixel forever.
+__device__ __forceinline__ uint32_t take_unit(uint32_t *ctr, int lane)
+{
+        const uint32_t old = atomicAdd(ctr, lane == 0 ? 1u : 0u);
+        return __builtin_amdgcn_readlane(old, 0);
+}
+
+// Persistent variant (uninstrumented, no per-sample outputs): 4-wave
+// workgroups sized to fill the chip once; every wave pulls quadrant units
+// from a per-XCD counter (blocks b, b+8, ... share an XCD and its L2; an
+// XCD's counter covers one contiguous slice of the tiles) and, once its own
+// slice is exhausted, from the other XCDs' counters (VRT_PERSIST_HELP).
+// One-wave workgroups top out at 16 resident waves per CU (the per-CU
+// workgroup limit); at VRT_PERSIST_WAVES_PER_EU = 5 this kernel keeps 5
+// waves per SIMD = 20 per CU resident, and a wave never waits for a
+// workgroup sibling.  The counters belong to this launch alone (WorkQueue,
+// vrt_internal.h): nothing is reset at the end.
+// kFastOnly (camera rays of a finite scene, decided on the host): only the
+// fast standard-range march is compiled in; a wave with a ray that needs the
+// exact path (a non-zero denormal direction component) appends its unit to
+// the launch's deferred list, which k_render_defer renders afterwards.
+// kNS > 0: the first kNS node records are staged in LDS (VRT_LDS_NODES).
 constexpr int kPersistBlock = 256;
 #ifndef VRT_PERSIST_WAVES_PER_EU
 #define VRT_PERSIST_WAVES_PER_EU 5
 #endif
+#ifndef VRT_PERSIST_HELP
+#define VRT_PERSIST_HELP 1
+#endif
+#ifndef VRT_LDS_NODES
+#define VRT_LDS_NODES 0
+#endif
+template <bool kFastOnly>
 __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_render_p(RenderParams p)
 {
+        constexpr int kNS = kFastOnly ? VRT_LDS_NODES : 0;
         __shared__ uint2 stk[kStack * kPersistBlock];
+        stage_nodes<kNS>(p.sc.nodes, p.sc.nnodes);
         const int tid = threadIdx.x, lane = tid & 63;
         const int units = p.tiles_this_rank * 4;
         const int xcd = blockIdx.x & 7;
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < (VRT_PERSIST_HELP ? 8 : 1); ++j) {
                 const int x = (xcd + j) & 7;
                 int lo, hi;
                 queue_range(units, x, lo, hi);
                 if (lo >= hi)
                         continue;
                 for (;;) {
-                        uint32_t u = 0;
-                        if (lane == 0)
-                                u = atomicAdd(p.q.ctr + x * kQueueStride, 1u);
-                        u = __builtin_amdgcn_readfirstlane(u) - p.q.base[x];
+                        const uint32_t u = take_unit(p.q.ctr + x * kQueueStride, lane) - p.q.base[x];
                         if (u >= (uint32_t)(hi - lo))
                                 break;
                         const int unit = lo + (int)u;
-                        render_unit<false, false, kPersistBlock>(p, unit >> 2, unit & 3, lane, stk + tid, nullptr,
-                                                                 nullptr);
+                        if (!render_unit<false, false, kPersistBlock, false, kFastOnly, kNS>(
+                                    p, unit >> 2, unit & 3, lane, stk + tid, nullptr, nullptr) &&
+                            lane == 0) {
+                                const uint32_t d = atomicAdd(p.q.defer, 1u);
+                                if (d < (uint32_t)kDeferCap)
+                                        p.q.defer[kDeferList + d] = (uint32_t)unit;
+                        }
                 }
         }
+}
+
+// The units k_render_p<true> deferred (normally none): one workgroup, the
+// general march (ray_march_dispatch).  More than kDeferCap deferred units:
+// every unit is rendered again here (the render is deterministic, so units
+// already written are rewritten with the same values).  The count is reset
+// for the queue slot's next launch.
+__global__ __launch_bounds__(kPersistBlock) void k_render_defer(RenderParams p)
+{
+        __shared__ uint2 stk[kStack * kPersistBlock];
+        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        const uint32_t n = __builtin_amdgcn_readfirstlane(p.q.defer[0]);
+        const uint32_t units = (uint32_t)p.tiles_this_rank * 4u;
+        const bool all = n > (uint32_t)kDeferCap;
+        const uint32_t m = all ? units : n;
+        for (uint32_t i = (uint32_t)wave; i < m; i += kPersistBlock / 64) {
+                const uint32_t unit = all ? i : __builtin_amdgcn_readfirstlane(p.q.defer[kDeferList + i]);
+                render_unit<false, false, kPersistBlock, false, false>(p, (int)(unit >> 2), (int)(unit & 3), lane,
+                                                                        stk + tid, nullptr, nullptr);
+        }
+        __syncthreads();
+        if (tid == 0)
+                p.q.defer[0] = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -1308,6 +1429,8 @@ struct SecondaryParams {
         float *vis;            // nx*ny, this rank's pixels written
         int32_t *s_hit, *s_tri;
         uint32_t *s_vox;
+        int32_t units;         // this rank's pixels (persistent launch)
+        WorkQueue q;           // persistent launch only
 };
 
 #ifndef VRT_SEC_WAVES
@@ -1318,17 +1441,16 @@ struct SecondaryParams {
 #endif
 constexpr int kSecBlock = 64 * VRT_SEC_WAVES;
 
+// One pixel of config 5: this rank's k-th pixel (chunks of 64 pixels dealt
+// round-robin over the ranks), the wave's 64 lanes = its secondary rays.
+// pts = this wave's 64 sphere points in LDS.
 // kAny (no per-ray ids requested): the visibility image needs only each
 // ray's hit boolean -> the occlusion walk (ray_occluded), same booleans.
-template <bool kR64, bool kAny>
-__global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(SecondaryParams p)
+template <bool kR64, bool kAny, int kS>
+__device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_t k, int lane, uint2 *stk,
+                                                float (*pts)[3])
 {
-        __shared__ uint2 stk[kStack * kSecBlock];
-        __shared__ float pts[VRT_SEC_WAVES][64][3];
-        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
         const int64_t npix = (int64_t)p.W8 * p.H8;
-        // this rank's k-th pixel: chunks of 64 pixels dealt round-robin
-        const int64_t k = (int64_t)blockIdx.x * VRT_SEC_WAVES + wave;
         const int64_t chunk = k >> 6;
         const int64_t pix = ((chunk * p.nranks + p.rank) << 6) + (k & 63);
         if (pix >= npix)
@@ -1336,7 +1458,11 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
         const int px = (int)(pix % p.W8), py = (int)(pix / p.W8);
         const float *pr = p.prim + 8 * pix;
         const size_t vi = (size_t)py * p.nx + px;
-        if (pr[0] == 0.f) {  // primary miss: the wave leaves together
+        // the pixel is wave-uniform: read its hit flag as a scalar so that
+        // the early exit is a uniform branch (a divergent exit inside the
+        // persistent loop of k_secondary_p is miscompiled into a loop that
+        // never takes another unit)
+        if (__builtin_amdgcn_readfirstlane(__float_as_uint(pr[0])) == 0u) {  // primary miss (+0.f)
                 if (lane == 0)
                         p.vis[vi] = 1.0f;
                 return;
@@ -1355,9 +1481,9 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
                 const uint64_t mask = __ballot(acc);
                 const int rk = have + (int)__popcll(mask & ((1ull << lane) - 1ull));
                 if (acc && rk < p.spp) {
-                        pts[wave][rk][0] = x;
-                        pts[wave][rk][1] = y;
-                        pts[wave][rk][2] = z;
+                        pts[rk][0] = x;
+                        pts[rk][1] = y;
+                        pts[rk][2] = z;
                 }
                 have += (int)__popcll(mask);
                 st = pcg_advance(st, 192);
@@ -1367,16 +1493,16 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         bool hit = false;
         if (lane < p.spp) {
-                const f3 pt = mk3(pts[wave][lane][0], pts[wave][lane][1], pts[wave][lane][2]);
+                const f3 pt = mk3(pts[lane][0], pts[lane][1], pts[lane][2]);
                 const f3 dn = normalize(nrm + pt);  // Ray{hit, n + p, res} normalises d
                 const RayK r = make_rayk(hp, dn, p.res, kFltMax);
                 const size_t si = vi * (size_t)p.spp + lane;
                 if (kAny) {
-                        hit = ray_occluded_dispatch<kSecBlock, kR64>(p.sc, r, stk + tid);
+                        hit = ray_occluded_dispatch<kS, kR64>(p.sc, r, stk);
                         if (p.s_hit) p.s_hit[si] = hit ? 1 : 0;
                 } else {
                         MarchResult m;
-                        ray_march_dispatch<false, kSecBlock, false, kR64>(p.sc, r, stk + tid, nullptr, nullptr, m);
+                        ray_march_dispatch<false, kS, false, kR64>(p.sc, r, stk, nullptr, nullptr, m);
                         hit = m.hit;
                         if (p.s_hit) p.s_hit[si] = m.hit ? 1 : 0;
                         if (p.s_tri) p.s_tri[si] = m.hit ? (int32_t)m.tri : -1;
@@ -1388,16 +1514,62 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
                 p.vis[vi] = (float)(p.spp - (int)__popcll(hm)) / (float)p.spp;
 }
 
+template <bool kR64, bool kAny>
+__global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(SecondaryParams p)
+{
+        __shared__ uint2 stk[kStack * kSecBlock];
+        __shared__ float pts[VRT_SEC_WAVES][64][3];
+        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        const int64_t k = (int64_t)blockIdx.x * VRT_SEC_WAVES + wave;
+        secondary_pixel<kR64, kAny, kSecBlock>(p, k, lane, stk + tid, pts[wave]);
+}
+
+// Persistent config 5: one resident generation of 4-wave workgroups; each
+// wave pulls one pixel at a time from the per-XCD counters of the launch's
+// WorkQueue (XCD x owns a contiguous slice of this rank's pixels, then
+// helps the others), so no wave waits for a slow pixel of a sibling and the
+// resident-wave count is not capped by the per-CU workgroup limit.
+constexpr int kSecPBlock = 256;
+#ifndef VRT_SECP_WAVES_PER_EU
+#define VRT_SECP_WAVES_PER_EU 6
+#endif
+template <bool kR64, bool kAny>
+__global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary_p(SecondaryParams p)
+{
+        __shared__ uint2 stk[kStack * kSecPBlock];
+        __shared__ float pts[kSecPBlock / 64][64][3];
+        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        const int units = p.units;
+        const int xcd = blockIdx.x & 7;
+        for (int j = 0; j < 8; ++j) {
+                const int x = (xcd + j) & 7;
+                int lo, hi;
+                queue_range(units, x, lo, hi);
+                if (lo >= hi)
+                        continue;
+                for (;;) {
+                        const uint32_t u = take_unit(p.q.ctr + x * kQueueStride, lane) - p.q.base[x];
+                        if (u >= (uint32_t)(hi - lo))
+                                break;
+                        secondary_pixel<kR64, kAny, kSecPBlock>(p, (int64_t)(lo + (int)u), lane, stk + tid,
+                                                                pts[wave]);
+                }
+        }
+}
+
 hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nranks, float res,
                             float *prim, float *vis, int32_t *s_hit, int32_t *s_tri,
-                            uint32_t *s_vox, hipStream_t st)
+                            uint32_t *s_vox, const WorkQueue *q, hipStream_t st, int *q_waves, int *q_units)
 {
+        *q_waves = 0;
+        *q_units = 0;
         const int64_t npix = (int64_t)rp.ntx * 8 * rp.nty * 8;
         if (npix <= 0)
                 return hipSuccess;
         hipLaunchKernelGGL(rp.sc.wide_leaves ? k_primary1<true> : k_primary1<false>, dim3((unsigned)((npix + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
                            rp, prim);
         SecondaryParams sp;
+        std::memset(&sp, 0, sizeof sp);
         sp.sc = rp.sc;
         sp.nx = rp.cam.nx;
         sp.W8 = rp.ntx * 8;
@@ -1419,8 +1591,20 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
 #define VRT_SEC_ANY 1
 #endif
         const bool any = VRT_SEC_ANY && !s_tri && !s_vox;
-        void (*kern)(SecondaryParams) = sp.sc.wide_leaves ? (any ? k_secondary<true, true> : k_secondary<true, false>)
-                                                          : (any ? k_secondary<false, true> : k_secondary<false, false>);
+        const bool w = sp.sc.wide_leaves != 0;
+        if (q && secondary_uses_queue(rp.sc) && waves <= INT_MAX) {
+                sp.units = (int32_t)waves;
+                sp.q = *q;
+                const int g = (int)std::min<int64_t>(rp.sc.sec_blocks, ((waves + 3) / 4 + 7) & ~7LL);
+                void (*kern)(SecondaryParams) = w ? (any ? k_secondary_p<true, true> : k_secondary_p<true, false>)
+                                                  : (any ? k_secondary_p<false, true> : k_secondary_p<false, false>);
+                hipLaunchKernelGGL(kern, dim3(g), dim3(kSecPBlock), 0, st, sp);
+                *q_waves = g * (kSecPBlock / 64);
+                *q_units = (int)waves;
+                return hipGetLastError();
+        }
+        void (*kern)(SecondaryParams) = w ? (any ? k_secondary<true, true> : k_secondary<true, false>)
+                                          : (any ? k_secondary<false, true> : k_secondary<false, false>);
         hipLaunchKernelGGL(kern, dim3((unsigned)((waves + VRT_SEC_WAVES - 1) / VRT_SEC_WAVES)), dim3(kSecBlock), 0,
                            st, sp);
         return hipGetLastError();
@@ -1539,42 +1723,97 @@ hipError_t launch_selftest_order(const float *dist, const uint32_t *hm, int64_t 
 #ifndef VRT_PERSIST
 #define VRT_PERSIST 1
 #endif
-// persistent waves for RefRec48 scenes; large-leaf (RefRec64) scenes keep
-// one-wave workgroups (-11 % persistent at depth 6)
-bool render_uses_queue(const DevScene &sc, bool instrumented)
+#ifndef VRT_PERSIST_FAST
+#define VRT_PERSIST_FAST 1
+#endif
+#ifndef VRT_SEC_PERSIST
+#define VRT_SEC_PERSIST 1
+#endif
+// persistent waves for RefRec48 scenes without per-sample outputs;
+// large-leaf (RefRec64) scenes keep one-wave workgroups (-11 % persistent at
+// depth 6).  The fast-only kernel when the camera makes standard-range
+// rays (tmin = +0, tmax = FLT_MAX) from a finite origin in a finite scene;
+// the kernel itself re-checks every wave and defers what is not exact.
+RenderKind render_kind(const RenderParams &p, bool instrumented)
 {
-        return VRT_PERSIST && !instrumented && !sc.wide_leaves && sc.persist_blocks > 0;
+        const SampleOut &so = p.so;
+        if (!VRT_PERSIST || instrumented || so.hit || so.tri || so.vox || so.rgb || so.cnt || p.sc.wide_leaves ||
+            p.sc.persist_blocks <= 0)
+                return kRenderGrid;
+        const CamParams &c = p.cam;
+        bool fast = VRT_PERSIST_FAST && p.sc.fast_ok && __builtin_bit_cast(uint32_t, c.tmin) == 0u &&
+                    c.tmax == kFltMax;
+        for (int k = 0; k < 3; ++k)
+                fast = fast && std::fabs(c.origin[k]) < 0x1p60f;
+        return fast ? kRenderPersistFast : kRenderPersist;
 }
 
-hipError_t persistent_render_blocks(int *blocks)
+bool secondary_uses_queue(const DevScene &sc)
 {
-        int per_cu = 0, dev = 0;
+        return VRT_SEC_PERSIST && sc.sec_blocks > 0;
+}
+
+static int resident_blocks(const void *kern, int block, const hipDeviceProp_t &prop, hipError_t *e)
+{
+        int per_cu = 0;
+        *e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, 0);
+        return std::max(8, (per_cu * prop.multiProcessorCount) & ~7);
+}
+
+hipError_t persistent_blocks(int *render_blocks, int *sec_blocks)
+{
+        int dev = 0;
         hipDeviceProp_t prop;
         hipError_t e = hipGetDevice(&dev);
         if (e == hipSuccess)
                 e = hipGetDeviceProperties(&prop, dev);
-        if (e == hipSuccess)
-                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_render_p, kPersistBlock, 0);
         if (e != hipSuccess)
                 return e;
-        *blocks = std::max(8, (per_cu * prop.multiProcessorCount) & ~7);
-        return hipSuccess;
+        // the smaller residency of the two render variants (a surplus block
+        // only waits, then finds the queues empty)
+        const int a = resident_blocks(reinterpret_cast<const void *>(k_render_p<true>), kPersistBlock, prop, &e);
+        if (e != hipSuccess)
+                return e;
+        const int b = resident_blocks(reinterpret_cast<const void *>(k_render_p<false>), kPersistBlock, prop, &e);
+        if (e != hipSuccess)
+                return e;
+        *render_blocks = std::min(a, b);
+        int sb = 1 << 30;
+        const void *sk[4] = { reinterpret_cast<const void *>(k_secondary_p<false, false>),
+                              reinterpret_cast<const void *>(k_secondary_p<false, true>),
+                              reinterpret_cast<const void *>(k_secondary_p<true, false>),
+                              reinterpret_cast<const void *>(k_secondary_p<true, true>) };
+        for (int i = 0; i < 4 && e == hipSuccess; ++i)
+                sb = std::min(sb, resident_blocks(sk[i], kSecPBlock, prop, &e));
+        *sec_blocks = sb;
+        return e;
 }
 
 hipError_t launch_render(const RenderParams &p, bool instrumented,
-                         hipStream_t st, int *queue_waves)
+                         hipStream_t st, int *q_waves, int *q_units)
 {
-        *queue_waves = 0;
+        *q_waves = 0;
+        *q_units = 0;
         if (p.tiles_this_rank <= 0)
                 return hipSuccess;
         const bool w = p.sc.wide_leaves != 0;
-        if (render_uses_queue(p.sc, instrumented)) {
+        const RenderKind kind = render_kind(p, instrumented);
+        if (kind != kRenderGrid) {
                 // one resident generation of 4-wave workgroups (<= one per
                 // 4 units, a multiple of 8 for the XCD map)
                 const int need = (p.tiles_this_rank + 7) & ~7;  // 4 units per tile, 4 waves per block
                 const int g = std::min(p.sc.persist_blocks, need);
-                hipLaunchKernelGGL(k_render_p, dim3(g), dim3(kPersistBlock), 0, st, p);
-                *queue_waves = g * (kPersistBlock / 64);
+                if (kind == kRenderPersistFast) {
+                        hipLaunchKernelGGL(k_render_p<true>, dim3(g), dim3(kPersistBlock), 0, st, p);
+                        hipLaunchKernelGGL(k_render_defer, dim3(1), dim3(kPersistBlock), 0, st, p);
+                } else {
+                        hipLaunchKernelGGL(k_render_p<false>, dim3(g), dim3(kPersistBlock), 0, st, p);
+                }
+                // failing adds per slice counter: every wave visits every
+                // slice (VRT_PERSIST_HELP), or only its own XCD's (g is a
+                // multiple of 8: g/8 blocks per XCD residue)
+                *q_waves = (VRT_PERSIST_HELP ? g : g / 8) * (kPersistBlock / 64);
+                *q_units = p.tiles_this_rank * 4;
                 return hipGetLastError();
         }
         // round the grid up to a multiple of 8 (one slot per XCD)
