@@ -36,6 +36,7 @@ N_CU = 256              # MI355X compute units (4 SIMD-32 each)
 # VALU issue peak: one wave64 VALU instruction per 2 cycles per SIMD
 # (MI355X_MICROARCH.md "Wave scheduling"), 4 SIMDs per CU
 VALU_WAVE_INSTR_PER_CYCLE = N_CU * 4 / 2
+MAX_CLOCK_GHZ = 2.4     # MI355X max engine clock (MI355X_MICROARCH.md chip table)
 
 
 def log(*a):
@@ -140,25 +141,33 @@ def run_pmc(a, kernel_prefix, save_dir=""):
 
 def roofline_from_pmc(pmc, kernel_ms, out_bytes, ref_bytes):
     """The measured roofline of the dominant kernel: VALU issue (the limiter,
-    DESIGN.md §4) with its peak at the clock measured in the same passes, and
-    HBM traffic (FETCH_SIZE x2 per MI355X_MICROARCH.md §HBM + WRITE_SIZE;
-    rocprofv3 reports KiB) as a fraction of the 8 TB/s peak."""
+    DESIGN.md §4) -- the VALU wave-instructions of one launch (SQ_INSTS_VALU)
+    over this run's HIP-event kernel time, against the issue peak at the max
+    engine clock -- and HBM traffic (FETCH_SIZE x2 per MI355X_MICROARCH.md
+    §HBM + WRITE_SIZE; rocprofv3 reports KiB) over the same time as a
+    fraction of the 8 TB/s peak.  issue_frac_at_clock is the same
+    instruction count over the issue slots of the cycles the profiled
+    launch actually ran (GRBM_GUI_ACTIVE / 8), i.e. at the measured clock."""
     m = pmc["means"]
     t = kernel_ms * 1e-3
     rd = 2 * m["FETCH_SIZE"] * 1024
     wr = m["WRITE_SIZE"] * 1024
     traffic = rd + wr
+    cycles = m["GRBM_GUI_ACTIVE"] / 8                          # summed over the 8 XCDs
     cms = pmc["child_kernel_ms"] or kernel_ms
-    clock = m["GRBM_GUI_ACTIVE"] / 8 / (cms * 1e-3) / 1e9  # GHz, summed over 8 XCDs
-    achieved = m["SQ_INSTS_VALU"] / t / 1e9                  # G wave-instr/s
-    peak = VALU_WAVE_INSTR_PER_CYCLE * clock                  # G wave-instr/s
+    clock = cycles / (cms * 1e-3) / 1e9                        # GHz in the profiled pass
+    achieved = m["SQ_INSTS_VALU"] / t / 1e9                    # G wave-instr/s
+    peak = VALU_WAVE_INSTR_PER_CYCLE * MAX_CLOCK_GHZ           # G wave-instr/s
     hbm = traffic / t / 1e9
     h, mi = m.get("TCC_HIT_sum", 0.0), m.get("TCC_MISS_sum", 0.0)
     return {
         "bound": "valu",
         "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "G wave-instr/s",
         "frac": round(achieved / peak, 4),
-        "peak_def": f"{N_CU} CUs x 4 SIMDs x 1/2 wave64 VALU instr/cycle x {clock:.3f} GHz (GRBM_GUI_ACTIVE/8/kernel time)",
+        "peak_def": f"{N_CU} CUs x 4 SIMDs x 1/2 wave64 VALU instr/cycle x {MAX_CLOCK_GHZ} GHz max clock",
+        "issue_frac_at_clock": round(m["SQ_INSTS_VALU"] / (VALU_WAVE_INSTR_PER_CYCLE * cycles), 4),
+        "clock_ghz_profiled": round(clock, 3),
+        "valu_instr_per_launch": round(m["SQ_INSTS_VALU"]),
         "traffic": round(traffic),
         "hbm": {"achieved": round(hbm, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(hbm / PEAK_HBM_GBS, 4),
                 "read_bytes": round(rd), "read_bytes_raw": round(rd / 2), "write_bytes": round(wr)},
@@ -342,7 +351,7 @@ def main():
         finish(b)
         if rank == 0:
             visb[b].zero_()  # the previous reduce summed into rank 0's buffer
-        # each rank writes only its own pixels (64-pixel chunks, round-robin);
+        # each rank writes only its own pixels (8x8 tiles dealt round-robin);
         # the others stay +0.0, so a SUM reduce assembles the image exactly
         tree.render_secondary_device(cam, film, a.spp, rank, world, prim.data_ptr(), visb[b].data_ptr(), sp)
         if timed:
@@ -605,7 +614,7 @@ def main():
                       f"(1 primary + {a.spp} stochastic secondary rays per hit pixel)")
             workload = (f"config 5: {a.width}x{a.height} primary hit + {a.spp} spp secondary rays, "
                         f"{scene_name} ({sd.ntri} tris), max_depth {a.depth}")
-            par = f"pixel chunks x{world}" + (f" + {coll} sum-reduce" if world > 1 else "")
+            par = f"pixel tiles x{world}" + (f" + {coll} sum-reduce" if world > 1 else "")
         else:
             total_rays = rays_per_frame * a.steps
             mean_rays = rays_per_frame

@@ -194,8 +194,8 @@ int vrt_render_secondary(vrt_scene *s, const vrt_camera *cam,
                          const vrt_film *film, int spp, float *vis,
                          int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox,
                          int64_t *rays);
-/* Device-resident variant: rank `rank` of `nranks` writes its pixels (64-
- * pixel chunks dealt round-robin) into d_vis (nx*ny floats, caller-zeroed:
+/* Device-resident variant: rank `rank` of `nranks` writes its pixels (the
+ * 8x8-pixel tiles t with t % nranks == rank) into d_vis (nx*ny floats, caller-zeroed:
  * a sum-reduce over ranks assembles the image exactly); d_prim = scratch of
  * 8*(nx/8)*8*(ny/8)*8 floats. */
 int vrt_render_secondary_device(vrt_scene *s, const vrt_camera *cam,

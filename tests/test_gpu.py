@@ -362,21 +362,30 @@ def test_secondary_occlusion_walk_matches_ordered_walk(proxy_small, depth):
         assert 0 < d["hit"].sum() < d["hit"].size  # both outcomes occur
 
 
-def test_secondary_rank_partition_sums_to_image(proxy_small):
+@pytest.mark.parametrize("nx,ny,nranks", [(72, 40, 3), (512, 40, 8)])
+def test_secondary_rank_partition_sums_to_image(proxy_small, nx, ny, nranks):
+    """Each rank writes exactly the pixels of its 8x8 tiles (dist.py
+    secondary_mask); the parts sum to the single-rank image.  512 px / 8
+    ranks: every rank's tiles form an exact grid 8 tiles wide, so the
+    persistent kernel's XCD strips are in use."""
     import torch
+    from voxelraytrace20190722_amd import dist as vd
     tree = vrt.VoxelOctree(proxy_small, 6)
     mn, mx = tree.root_box
     fov, eye, spot, up = vrt.sweep_pose(mn, mx, 4, 16)
     cam = vrt.Camera(fov, eye, spot, up)
-    film = vrt.Film(1, 1, 72, 40)
+    film = vrt.Film(1, 1, nx, ny)
     ref, _ = tree.render_secondary(cam, film, spp=64)
     dev = torch.device("cuda:0")
-    prim = torch.zeros(72 * 40 * 8, dtype=torch.float32, device=dev)
-    acc = torch.zeros((40, 72), dtype=torch.float32, device=dev)
-    for r in range(3):
-        part = torch.zeros((40, 72), dtype=torch.float32, device=dev)
-        tree.render_secondary_device(cam, film, 64, r, 3, prim.data_ptr(), part.data_ptr(), None)
+    prim = torch.zeros(nx * ny * 8, dtype=torch.float32, device=dev)
+    acc = torch.zeros((ny, nx), dtype=torch.float32, device=dev)
+    for r in range(nranks):
+        part = torch.zeros((ny, nx), dtype=torch.float32, device=dev)
+        tree.render_secondary_device(cam, film, 64, r, nranks, prim.data_ptr(), part.data_ptr(), None)
         torch.cuda.synchronize()
+        m = vd.secondary_mask(nx, ny, r, nranks)
+        pa = part.cpu().numpy()
+        assert np.all(pa[~m] == 0) and np.all(pa[m] > 0) == np.all(ref[m] > 0)
         acc += part
     assert np.array_equal(bits(acc.cpu().numpy()), bits(ref))
 

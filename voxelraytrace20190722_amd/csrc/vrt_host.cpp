@@ -963,14 +963,11 @@ static int queue_take(vrt_scene *s, hipStream_t st, WorkQueue *q, int *slot)
         return VRT_OK;
 }
 
-static int queue_release(vrt_scene *s, int slot, hipStream_t st, int units, int waves)
+static int queue_release(vrt_scene *s, int slot, hipStream_t st, const int slice_units[8], int waves)
 {
-        for (int x = 0; x < 8; ++x) {
-                int lo, hi;
-                queue_range(units, x, lo, hi);
-                if (hi > lo)
-                        s->q_base[slot][x] += (uint32_t)(hi - lo) + (uint32_t)waves;
-        }
+        for (int x = 0; x < 8; ++x)
+                if (slice_units[x] > 0)
+                        s->q_base[slot][x] += (uint32_t)slice_units[x] + (uint32_t)waves;
         HIPCHK(hipEventRecord(s->q_ev[slot], st));
         s->q_live[slot] = true;
         return VRT_OK;
@@ -983,8 +980,8 @@ static int render_launch(vrt_scene *s, RenderParams &p, bool instrumented, hipSt
         if (render_kind(p, instrumented) != kRenderGrid)
                 if (int rc = queue_take(s, st, &p.q, &slot))
                         return rc;
-        int waves = 0, units = 0;
-        HIPCHK(launch_render(p, instrumented, st, &waves, &units));
+        int waves = 0, units[8];
+        HIPCHK(launch_render(p, instrumented, st, &waves, units));
         if (slot >= 0)
                 return queue_release(s, slot, st, units, waves);
         return VRT_OK;
@@ -1001,9 +998,9 @@ static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int ra
         if (secondary_uses_queue(p.sc))
                 if (int rc = queue_take(s, st, &q, &slot))
                         return rc;
-        int waves = 0, units = 0;
+        int waves = 0, units[8];
         HIPCHK(launch_secondary(p, spp, rank, nranks, scene_res(s), d_prim, d_vis, s_hit, s_tri, s_vox,
-                                slot >= 0 ? &q : nullptr, st, &waves, &units));
+                                slot >= 0 ? &q : nullptr, st, &waves, units));
         if (slot >= 0)
                 return queue_release(s, slot, st, units, waves);
         return VRT_OK;

@@ -128,6 +128,52 @@ __host__ __device__ inline void queue_range(int units, int x, int &lo, int &hi)
                 hi = lo;
 }
 
+// Unit order of a persistent launch: 2^sh units per 8x8-pixel tile (the 4
+// quadrants of a primary render, the 64 pixels of a config-5 launch).  When
+// this rank's tiles form an exact grid (vw columns x rows: one rank, or a
+// column count divisible by the ranks), XCD slice x is the vertical strip of
+// tile columns [x*vw/8, (x+1)*vw/8), numbered row-major inside the strip,
+// so the units one XCD runs at a time cover a compact screen region (its L2
+// serves one part of the octree).  Otherwise slice x is the contiguous
+// range queue_range() gives.  The host uses the same functions for the
+// queue bases.
+#ifndef VRT_STRIPS
+#define VRT_STRIPS 0
+#endif
+struct UnitMap {
+        int units, vw, rows, sh;
+        bool strips;
+};
+__host__ __device__ inline UnitMap unit_map(int ntx, int nty, int nranks, int tiles, int sh)
+{
+        UnitMap m;
+        m.units = tiles << sh;
+        m.vw = ntx / nranks;
+        m.rows = nty;
+        m.sh = sh;
+        m.strips = VRT_STRIPS && ntx % nranks == 0 && m.vw * nty == tiles && m.vw >= 8;
+        return m;
+}
+__host__ __device__ inline void slice_range(const UnitMap &m, int x, int &lo, int &hi)
+{
+        if (m.strips) {
+                lo = (m.rows * (x * m.vw / 8)) << m.sh;
+                hi = (m.rows * ((x + 1) * m.vw / 8)) << m.sh;
+        } else {
+                queue_range(m.units, x, lo, hi);
+        }
+}
+// unit `unit` of slice x (lo = its first unit) -> rank-local tile k << sh |
+// the unit's index inside the tile
+__host__ __device__ inline int unit_tile_sub(const UnitMap &m, int x, int unit, int lo)
+{
+        if (!m.strips)
+                return unit;
+        const int c0 = x * m.vw / 8, sw = (x + 1) * m.vw / 8 - c0;
+        const int j = (unit - lo) >> m.sh;
+        return (((j / sw) * m.vw + c0 + j % sw) << m.sh) | (unit & ((1 << m.sh) - 1));
+}
+
 // Camera + film constants for ray generation (T1), computed on the host.
 struct CamParams {
         float s[3], u[3], nf[3], e[3];  // columns of C_
@@ -222,11 +268,11 @@ hipError_t build_tree_device(int device, const float *pos, int ntri, const float
 // persistent kinds take their units from p.q.
 enum RenderKind { kRenderGrid = 0, kRenderPersist = 1, kRenderPersistFast = 2 };
 RenderKind render_kind(const RenderParams &p, bool instrumented);
-// *q_waves / *q_units = the failing adds each slice counter receives (the
-// waves launched that visit it) and the units queued (0 when no work queue
-// was used), for the queue bases
+// *q_waves = the failing adds each slice counter receives (the waves
+// launched that visit it), slice_units[x] = the units of slice x (all 0 when
+// no work queue was used), for the queue bases
 hipError_t launch_render(const RenderParams &p, bool instrumented,
-                         hipStream_t st, int *q_waves, int *q_units);
+                         hipStream_t st, int *q_waves, int slice_units[8]);
 // resident blocks of the persistent render / secondary kernels on the
 // current device
 hipError_t persistent_blocks(int *render_blocks, int *sec_blocks);
@@ -241,7 +287,7 @@ hipError_t launch_unpack(int nx, int ny, int ntx, int nty, int nranks,
 hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,
                             int nranks, float res, float *prim, float *vis,
                             int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox,
-                            const WorkQueue *q, hipStream_t st, int *q_waves, int *q_units);
+                            const WorkQueue *q, hipStream_t st, int *q_waves, int slice_units[8]);
 hipError_t launch_light(const LightParams &p, hipStream_t st);
 // samp: n x 6 floats followed by room for their sorted copy (n x 6);
 // seg_start: max_seg entries (>= non-empty leaves), nseg zeroed

@@ -1088,6 +1088,11 @@ template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly =
 __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wave, int lane, uint2 *stk,
                                             uint32_t *stk_aux, uint32_t *path_rem)
 {
+        // the lane id is re-read per unit (volatile asm: not hoisted out of
+        // a persistent loop), so its derived per-lane constants are
+        // recomputed instead of being held -- and spilled -- across units
+        if (!kSamples)
+                asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
         const int t = p.rank + k * p.nranks;
         const int tx = t % p.ntx, ty = t / p.ntx;
         const int s = lane & 3, pix = lane >> 2;
@@ -1202,8 +1207,10 @@ __global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k
 // one atomic) and the wave reads lane 0's result.  No lane-0-only branch
 // around the atomic: inside k_secondary_p's persistent loop that divergent
 // region was structurized into a loop that re-ran one pixel forever.
-__device__ __forceinline__ uint32_t take_unit(uint32_t *ctr, int lane)
+__device__ __forceinline__ uint32_t take_unit(uint32_t *ctr)
 {
+        int lane;  // read here, not held across the persistent loop
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
         const uint32_t old = atomicAdd(ctr, lane == 0 ? 1u : 0u);
         return __builtin_amdgcn_readlane(old, 0);
 }
@@ -1240,25 +1247,25 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
         __shared__ uint2 stk[kStack * kPersistBlock];
         stage_nodes<kNS>(p.sc.nodes, p.sc.nnodes);
         const int tid = threadIdx.x, lane = tid & 63;
-        const int units = p.tiles_this_rank * 4;
+        const UnitMap um = unit_map(p.ntx, p.nty, p.nranks, p.tiles_this_rank, 2);
         const int xcd = blockIdx.x & 7;
         for (int j = 0; j < (VRT_PERSIST_HELP ? 8 : 1); ++j) {
                 const int x = (xcd + j) & 7;
                 int lo, hi;
-                queue_range(units, x, lo, hi);
+                slice_range(um, x, lo, hi);
                 if (lo >= hi)
                         continue;
                 for (;;) {
-                        const uint32_t u = take_unit(p.q.ctr + x * kQueueStride, lane) - p.q.base[x];
+                        const uint32_t u = take_unit(p.q.ctr + x * kQueueStride) - p.q.base[x];
                         if (u >= (uint32_t)(hi - lo))
                                 break;
-                        const int unit = lo + (int)u;
+                        const int kq = unit_tile_sub(um, x, lo + (int)u, lo);
                         if (!render_unit<false, false, kPersistBlock, false, kFastOnly, kNS>(
-                                    p, unit >> 2, unit & 3, lane, stk + tid, nullptr, nullptr) &&
+                                    p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr) &&
                             lane == 0) {
                                 const uint32_t d = atomicAdd(p.q.defer, 1u);
                                 if (d < (uint32_t)kDeferCap)
-                                        p.q.defer[kDeferList + d] = (uint32_t)unit;
+                                        p.q.defer[kDeferList + d] = (uint32_t)kq;
                         }
                 }
         }
@@ -1423,7 +1430,7 @@ __global__ __launch_bounds__(kBlock) void k_primary1(RenderParams p, float *__re
 struct SecondaryParams {
         DevScene sc;
         int32_t nx, W8, H8, spp;
-        int32_t rank, nranks;  // pixel p handled when (p / 64) % nranks == rank
+        int32_t rank, nranks;  // 8x8 tile t handled when t % nranks == rank
         float res;
         const float *prim;
         float *vis;            // nx*ny, this rank's pixels written
@@ -1441,8 +1448,8 @@ struct SecondaryParams {
 #endif
 constexpr int kSecBlock = 64 * VRT_SEC_WAVES;
 
-// One pixel of config 5: this rank's k-th pixel (chunks of 64 pixels dealt
-// round-robin over the ranks), the wave's 64 lanes = its secondary rays.
+// One pixel of config 5: this rank's k-th pixel (pixel k % 64 of its tile
+// k / 64), the wave's 64 lanes = its secondary rays.
 // pts = this wave's 64 sphere points in LDS.
 // kAny (no per-ray ids requested): the visibility image needs only each
 // ray's hit boolean -> the occlusion walk (ray_occluded), same booleans.
@@ -1450,12 +1457,17 @@ template <bool kR64, bool kAny, int kS>
 __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_t k, int lane, uint2 *stk,
                                                 float (*pts)[3])
 {
-        const int64_t npix = (int64_t)p.W8 * p.H8;
-        const int64_t chunk = k >> 6;
-        const int64_t pix = ((chunk * p.nranks + p.rank) << 6) + (k & 63);
-        if (pix >= npix)
+        // lane id re-read per pixel (not held across k_secondary_p's loop)
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        // this rank's tile kt = k / 64 (8x8-pixel tiles dealt round-robin:
+        // tile t -> rank t % nranks, as the primary render), pixel k % 64
+        // of it, row-major
+        const int ntx = p.W8 >> 3;
+        const int64_t t = (k >> 6) * p.nranks + p.rank;
+        if (t >= (int64_t)ntx * (p.H8 >> 3))
                 return;
-        const int px = (int)(pix % p.W8), py = (int)(pix / p.W8);
+        const int px = (int)(t % ntx) * 8 + (int)(k & 7), py = (int)(t / ntx) * 8 + (int)((k >> 3) & 7);
+        const int64_t pix = (int64_t)py * p.W8 + px;
         const float *pr = p.prim + 8 * pix;
         const size_t vi = (size_t)py * p.nx + px;
         // the pixel is wave-uniform: read its hit flag as a scalar so that
@@ -1539,30 +1551,31 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
         __shared__ uint2 stk[kStack * kSecPBlock];
         __shared__ float pts[kSecPBlock / 64][64][3];
         const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-        const int units = p.units;
+        const UnitMap um = unit_map(p.W8 >> 3, p.H8 >> 3, p.nranks, p.units >> 6, 6);
         const int xcd = blockIdx.x & 7;
         for (int j = 0; j < 8; ++j) {
                 const int x = (xcd + j) & 7;
                 int lo, hi;
-                queue_range(units, x, lo, hi);
+                slice_range(um, x, lo, hi);
                 if (lo >= hi)
                         continue;
                 for (;;) {
-                        const uint32_t u = take_unit(p.q.ctr + x * kQueueStride, lane) - p.q.base[x];
+                        const uint32_t u = take_unit(p.q.ctr + x * kQueueStride) - p.q.base[x];
                         if (u >= (uint32_t)(hi - lo))
                                 break;
-                        secondary_pixel<kR64, kAny, kSecPBlock>(p, (int64_t)(lo + (int)u), lane, stk + tid,
-                                                                pts[wave]);
+                        secondary_pixel<kR64, kAny, kSecPBlock>(p, (int64_t)unit_tile_sub(um, x, lo + (int)u, lo),
+                                                                lane, stk + tid, pts[wave]);
                 }
         }
 }
 
 hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nranks, float res,
                             float *prim, float *vis, int32_t *s_hit, int32_t *s_tri,
-                            uint32_t *s_vox, const WorkQueue *q, hipStream_t st, int *q_waves, int *q_units)
+                            uint32_t *s_vox, const WorkQueue *q, hipStream_t st, int *q_waves, int slice_units[8])
 {
         *q_waves = 0;
-        *q_units = 0;
+        for (int x = 0; x < 8; ++x)
+                slice_units[x] = 0;
         const int64_t npix = (int64_t)rp.ntx * 8 * rp.nty * 8;
         if (npix <= 0)
                 return hipSuccess;
@@ -1583,10 +1596,12 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
         sp.s_hit = s_hit;
         sp.s_tri = s_tri;
         sp.s_vox = s_vox;
-        // pixels of this rank: whole 64-pixel chunks dealt round-robin
-        const int64_t chunks = (npix + 63) / 64;
-        const int64_t mine = (chunks - rank + nranks - 1) / nranks;
+        // pixels of this rank: its 8x8 tiles (tile t -> rank t % nranks)
+        const int64_t ntiles = npix / 64;
+        const int64_t mine = rank < ntiles ? (ntiles - rank + nranks - 1) / nranks : 0;
         const int64_t waves = mine * 64;
+        if (waves == 0)
+                return hipGetLastError();
 #ifndef VRT_SEC_ANY
 #define VRT_SEC_ANY 1
 #endif
@@ -1600,7 +1615,12 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                                                   : (any ? k_secondary_p<false, true> : k_secondary_p<false, false>);
                 hipLaunchKernelGGL(kern, dim3(g), dim3(kSecPBlock), 0, st, sp);
                 *q_waves = g * (kSecPBlock / 64);
-                *q_units = (int)waves;
+                const UnitMap um = unit_map(rp.ntx, rp.nty, nranks, (int)mine, 6);
+                for (int x = 0; x < 8; ++x) {
+                        int lo, hi;
+                        slice_range(um, x, lo, hi);
+                        slice_units[x] = hi - lo;
+                }
                 return hipGetLastError();
         }
         void (*kern)(SecondaryParams) = w ? (any ? k_secondary<true, true> : k_secondary<true, false>)
@@ -1790,10 +1810,11 @@ hipError_t persistent_blocks(int *render_blocks, int *sec_blocks)
 }
 
 hipError_t launch_render(const RenderParams &p, bool instrumented,
-                         hipStream_t st, int *q_waves, int *q_units)
+                         hipStream_t st, int *q_waves, int slice_units[8])
 {
         *q_waves = 0;
-        *q_units = 0;
+        for (int x = 0; x < 8; ++x)
+                slice_units[x] = 0;
         if (p.tiles_this_rank <= 0)
                 return hipSuccess;
         const bool w = p.sc.wide_leaves != 0;
@@ -1813,7 +1834,12 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 // slice (VRT_PERSIST_HELP), or only its own XCD's (g is a
                 // multiple of 8: g/8 blocks per XCD residue)
                 *q_waves = (VRT_PERSIST_HELP ? g : g / 8) * (kPersistBlock / 64);
-                *q_units = p.tiles_this_rank * 4;
+                const UnitMap um = unit_map(p.ntx, p.nty, p.nranks, p.tiles_this_rank, 2);
+                for (int x = 0; x < 8; ++x) {
+                        int lo, hi;
+                        slice_range(um, x, lo, hi);
+                        slice_units[x] = hi - lo;
+                }
                 return hipGetLastError();
         }
         // round the grid up to a multiple of 8 (one slot per XCD)

@@ -11,9 +11,9 @@ Primary frames: the render area is 8x8-pixel tiles t = ty*ntx + tx (ntx =
 nx//8, nty = ny//8); tile t belongs to rank t % nranks; a rank's buffer holds
 its tiles in order k = 0.. (t = rank + k*nranks), 64 pixels each, row-major
 inside the tile, 3 floats per pixel, `tiles_per_rank * 192` floats (unused
-tail zero).  Secondary frames (config 5): render-area pixels p = py*W8 + px
-in chunks of 64, chunk c belongs to rank c % nranks; every rank writes only
-its own pixels of a zeroed image, so a SUM reduce re-assembles it exactly.
+tail zero).  Secondary frames (config 5): the same tile deal (tile t ->
+rank t % nranks); every rank writes only the pixels of its tiles into a
+zeroed image, so a SUM reduce re-assembles it exactly.
 """
 import numpy as np
 
@@ -61,9 +61,9 @@ def unpack_tiles_host(gathered, nx, ny, nranks):
 
 def secondary_mask(nx, ny, rank, nranks):
     """(ny, nx) bool: the pixels `rank` computes in a config-5 frame."""
-    W8, H8 = 8 * (nx // 8), 8 * (ny // 8)
-    p = np.arange(W8 * H8)
-    mine = ((p >> 6) % nranks) == rank
+    ntx, nty = tile_grid(nx, ny)
+    t = np.arange(ntx * nty).reshape(nty, ntx)
+    mine = np.repeat(np.repeat((t % nranks) == rank, 8, 0), 8, 1)
     m = np.zeros((ny, nx), bool)
-    m[:H8, :W8] = mine.reshape(H8, W8)
+    m[:nty * 8, :ntx * 8] = mine
     return m
