@@ -66,6 +66,34 @@ def workload_args(a):
     return out
 
 
+def pmc_means(out_dir, kernel_prefix, steps):
+    """Per-dispatch means of every counter in the rocprofv3
+    *counter_collection.csv files under out_dir, over the last `steps`
+    dispatches of the kernel whose name contains kernel_prefix (the timed
+    ones; helper kernels excluded) -> (means, dispatch info) or (None, None)."""
+    import csv
+    rows = []
+    for root, _, files in os.walk(out_dir):
+        for f in files:
+            if f.endswith("counter_collection.csv"):
+                rows += list(csv.DictReader(open(os.path.join(root, f))))
+    per_disp, meta = {}, {}
+    for r in rows:
+        kn = r["Kernel_Name"]
+        if kernel_prefix not in kn or any(x in kn for x in ("k_render_defer", "k_primary1", "k_unpack")):
+            continue
+        d = per_disp.setdefault(int(r["Dispatch_Id"]), {})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        meta = {"kernel": kn, "grid": int(r["Grid_Size"]), "wg": int(r["Workgroup_Size"]),
+                "lds": int(r["LDS_Block_Size"]), "vgpr": int(r["VGPR_Count"]),
+                "sgpr": int(r["SGPR_Count"]), "scratch": int(r["Scratch_Size"])}
+    ids = sorted(per_disp)[-steps:]
+    if len(ids) < steps:
+        return None, None
+    names = sorted({c for i in ids for c in per_disp[i]})
+    return {c: float(np.mean([per_disp[i].get(c, 0.0) for i in ids])) for c in names}, meta
+
+
 def run_pmc(a, kernel_prefix, save_dir=""):
     """Run the timed region of this workload (warm-up 0, the same `steps`
     frames, so the same pose mix) once per counter group under rocprofv3
@@ -73,7 +101,6 @@ def run_pmc(a, kernel_prefix, save_dir=""):
     over the kernel's last `steps` dispatches (the timed ones) plus the
     child's own kernel time.  None if rocprofv3 is unavailable or a pass
     fails (the bench line then says so)."""
-    import csv
     import shutil
     import signal
     import subprocess
@@ -105,28 +132,12 @@ def run_pmc(a, kernel_prefix, save_dir=""):
         line = [ln for ln in so.splitlines() if ln.startswith("{")]
         if line:
             child_ms[name] = json.loads(line[-1]).get("kernel_ms_mean")
-        rows = []
-        for root, _, files in os.walk(out_dir):
-            for f in files:
-                if f.endswith("counter_collection.csv"):
-                    rows += list(csv.DictReader(open(os.path.join(root, f))))
-        per_disp = {}
-        for r in rows:
-            kn = r["Kernel_Name"]
-            if kernel_prefix not in kn or any(x in kn for x in ("k_render_defer", "k_primary1", "k_unpack")):
-                continue
-            d = int(r["Dispatch_Id"])
-            per_disp.setdefault(d, {})[r["Counter_Name"]] = per_disp.get(d, {}).get(r["Counter_Name"], 0.0) + \
-                float(r["Counter_Value"])
-            meta = {"kernel": r["Kernel_Name"], "grid": int(r["Grid_Size"]), "wg": int(r["Workgroup_Size"]),
-                    "lds": int(r["LDS_Block_Size"]), "vgpr": int(r["VGPR_Count"]),
-                    "sgpr": int(r["SGPR_Count"]), "scratch": int(r["Scratch_Size"])}
-        ids = sorted(per_disp)[-a.steps:]
-        if len(ids) < a.steps:
-            return None, f"pmc pass {name}: {len(ids)} dispatches of {kernel_prefix}, want {a.steps}"
-        for c in counters:
-            means[c] = float(np.mean([per_disp[i].get(c, 0.0) for i in ids]))
-        log(f"[pmc] pass {name}: {len(ids)} dispatches, {time.time() - t0:.1f} s")
+        got, meta_ = pmc_means(out_dir, kernel_prefix, a.steps)
+        if got is None:
+            return None, f"pmc pass {name}: fewer than {a.steps} dispatches of {kernel_prefix}"
+        means.update(got)
+        meta = meta_
+        log(f"[pmc] pass {name}: {a.steps} dispatches, {time.time() - t0:.1f} s")
         if save_dir:
             os.makedirs(save_dir, exist_ok=True)
             for root, _, files in os.walk(out_dir):

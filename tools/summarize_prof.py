@@ -3,7 +3,8 @@
   profiles/TAG_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
   profiles/TAG_summary.json       per-dispatch means of every PMC counter for
                                   the render kernel + derived figures
-and update profiles/pmc_traffic.json (HBM bytes per launch, read by bench.py).
+(bench.py measures its roofline live with its own PMC passes; this tool
+summarises the separate tools/prof.sh runs.)
 
 FETCH_SIZE / WRITE_SIZE are KiB.  MI355X_MICROARCH.md §HBM: on gfx950
 FETCH_SIZE reads 1/2 of the bytes of a wide coalesced stream; other access
@@ -77,19 +78,6 @@ def main():
         der["avg_waves_per_cu"] = 4 * mean["SQ_WAVE_CYCLES"] / (mean["GRBM_GUI_ACTIVE"] / 8) / 256
     out["derived"] = der
     json.dump(out, open(os.path.join(dst, f"{a.tag}_summary.json"), "w"), indent=1)
-    if "hbm_bytes_per_launch" in der:
-        tj_path = os.path.join(dst, "pmc_traffic.json")
-        tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
-        tj[a.key] = round(der["hbm_bytes_per_launch"])
-        json.dump(tj, open(tj_path, "w"), indent=1, sort_keys=True)
-    # the measured bound next to the algorithmic roofline (bench.py reports it)
-    dj_path = os.path.join(dst, "pmc_derived.json")
-    dj = json.load(open(dj_path)) if os.path.exists(dj_path) else {}
-    keep = ("hbm_bytes_per_launch", "hbm_GBps", "l2_hit_rate", "valu_issue_frac", "valu_per_wave",
-            "avg_waves_per_cu", "clock_GHz")
-    dj[a.key] = {k: round(der[k], 4) for k in keep if k in der}
-    dj[a.key]["source"] = f"profiles/{a.tag}_summary.json"
-    json.dump(dj, open(dj_path, "w"), indent=1, sort_keys=True)
     print(json.dumps(out, indent=1))
 
 
