@@ -98,6 +98,29 @@ __device__ __forceinline__ void load_node_st(const NodeRec *__restrict__ nodes, 
 }
 
 // ---------------------------------------------------------------------------
+// Diagnostic build only (VRT_PHASE_STAMPS=1, never the product): per-wave
+// phase cycles (s_memtime) and lane activity of the fast march, summed over
+// all waves into g_phase (read by vrt_diag_phases).
+#ifndef VRT_PHASE_STAMPS
+#define VRT_PHASE_STAMPS 0
+#endif
+#if VRT_PHASE_STAMPS
+__device__ unsigned long long g_phase[16];
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+        for (int o = 32; o > 0; o >>= 1)
+                v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+        return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+        for (int o = 32; o > 0; o >>= 1)
+                v += (uint32_t)__shfl_xor((int)v, o, 64);
+        return v;
+}
+#endif
+
+// ---------------------------------------------------------------------------
 // travorder's child order (VRT/voxel_octree.cc:77-97): std::sort of the 8
 // Items {ci, dist} with `lhs.dist < rhs.dist`.  For 8 elements libstdc++'s
 // std::sort is one __insertion_sort (the introsort loop stops at 16
@@ -360,10 +383,17 @@ __device__ __forceinline__ uint32_t expand_v1(const float bmin[3],
 // children ordered by two_slot_order / net4_order when no lane of the wave
 // has more than 2 / 4 of them (rank_order8 otherwise); the travorder
 // distances are finished only when some lane orders >= 2 children.
-// kStd: every lane's ray has tmin == +0 and tmax == FLT_MAX, so (fast path,
-// no NaN) `t >= tmin && t <= tmax` is exactly "t is +-0, +subnormal or
+// kStd >= 1: every lane's ray has tmin == +0 and tmax == FLT_MAX, so (fast
+// path, no NaN) `t >= tmin && t <= tmax` is exactly "t is +-0, +subnormal or
 // +normal" -- one v_cmp_class instead of two compares and an AND.
-template <bool kStd>
+// kStd == 2: in addition every |dinv| <= 2^64 (no zero or tiny direction
+// component), so with |plane - o| < 2^61 (fast_ok) every slab distance is
+// finite and the reference's test !(t0 > t1) && (t0 in [0, FLT_MAX] ||
+// t1 in [0, FLT_MAX]) is exactly t0 <= t1 && t1 >= 0 (the second clause
+// follows from t1 >= 0 when t0 <= t1, and neither endpoint can be +inf),
+// i.e. max(t0, 0) <= t1: the 0 is folded into one axis's near distances
+// once per expansion, leaving max3, min3 and one compare per child.
+template <int kStd>
 __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float bmax[3], const RayK &r, int &cnt,
                                               uint32_t content)
 {
@@ -391,6 +421,10 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
                 nr[k][1] = fminf(tb, tc);
                 fr[k][1] = fmaxf(tb, tc);
         }
+        if (kStd == 2) {
+                nr[2][0] = fmaxf(nr[2][0], 0.0f);
+                nr[2][1] = fmaxf(nr[2][1], 0.0f);
+        }
         uint32_t hm = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -400,15 +434,20 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
                 float t0, t1;
                 asm("v_max3_f32 %0, %1, %2, %3" : "=v"(t0) : "v"(nr[0][mx]), "v"(nr[1][my]), "v"(nr[2][mz]));
                 asm("v_min3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(fr[0][mx]), "v"(fr[1][my]), "v"(fr[2][mz]));
-                bool in0, in1;
-                if (kStd) {
-                        in0 = __builtin_amdgcn_classf(t0, 0x1E0);  // -0, +0, +subnormal, +normal
-                        in1 = __builtin_amdgcn_classf(t1, 0x1E0);
+                bool h;
+                if (kStd == 2) {
+                        h = t0 <= t1;  // t0 = max(near distances, 0)
                 } else {
-                        in0 = (t0 >= r.tmin) & (t0 <= r.tmax);
-                        in1 = (t1 >= r.tmin) & (t1 <= r.tmax);
+                        bool in0, in1;
+                        if (kStd) {
+                                in0 = __builtin_amdgcn_classf(t0, 0x1E0);  // -0, +0, +subnormal, +normal
+                                in1 = __builtin_amdgcn_classf(t1, 0x1E0);
+                        } else {
+                                in0 = (t0 >= r.tmin) & (t0 <= r.tmax);
+                                in1 = (t1 >= r.tmin) & (t1 <= r.tmax);
+                        }
+                        h = !(t0 > t1) & (in0 | in1);
                 }
-                const bool h = !(t0 > t1) & (in0 | in1);
                 hm |= (uint32_t)h << i;
         }
         hm &= content;
@@ -443,7 +482,7 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
         return net4_order(dist_of, hm);
 }
 
-template <bool kFullPos, bool kFast, bool kStd = false>
+template <bool kFullPos, bool kFast, int kStd = 0>
 __device__ __forceinline__ uint32_t expand(const float bmin[3],
                                            const float bmax[3],
                                            const RayK &r, int &cnt,
@@ -604,7 +643,7 @@ __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, u
 
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).
-template <bool kCount, bool kFast, int kS, bool kStd, bool kUni, bool kR64, int kNS = 0>
+template <bool kCount, bool kFast, int kS, int kStd, bool kUni, bool kR64, int kNS = 0>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint2 *stk,
                                           uint32_t *stk_aux,
@@ -643,10 +682,20 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         // while-while: every lane first advances (pop / expand) to its next
         // non-empty leaf in DFS order, then the lanes test their leaves
         // together -- expand and leaf code no longer interleave per lane.
+#if VRT_PHASE_STAMPS
+        uint32_t d_it = 0, d_lp = 0, d_tri = 0, d_lpmax = 0, d_lpsum = 0, d_phmax = 0;
+        unsigned long long d_tin = 0, d_tleaf = 0;
+#endif
         for (;;) {
                 bool leaf = false;
                 uint32_t node = 0, nref = 0;
+#if VRT_PHASE_STAMPS
+                const unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
+#endif
                 for (;;) {
+#if VRT_PHASE_STAMPS
+                        ++d_it;
+#endif
                         if (cnt == 0) {
                                 if (sp == 0)
                                         break;
@@ -691,14 +740,71 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         leaf = true;
                         break;
                 }
+#if VRT_PHASE_STAMPS
+                const unsigned long long d_t1 = __builtin_amdgcn_s_memtime();
+                d_tin += d_t1 - d_t0;
+                {
+                        // over the lanes with a leaf (inactive lanes take no part)
+                        d_lpmax = 0;
+                        uint64_t lm = __ballot(leaf);
+                        while (lm) {
+                                const int l = __ffsll((long long)lm) - 1;
+                                const uint32_t v = __builtin_amdgcn_readlane(nref, l);
+                                d_lpmax = d_lpmax > v ? d_lpmax : v;  // this phase's longest leaf
+                                d_lpsum += v;
+                                lm &= lm - 1;
+                        }
+                        d_phmax += d_lpmax;
+                }
+#endif
                 if (!leaf)
                         break;
-                if (leaf_isect<kCount, kUni, kR64>(sc, b, nref, r, m)) {
+#if VRT_PHASE_STAMPS
+                ++d_lp;
+                d_tri += nref;
+#endif
+                const bool lh = leaf_isect<kCount, kUni, kR64>(sc, b, nref, r, m);
+#if VRT_PHASE_STAMPS
+                d_tleaf += __builtin_amdgcn_s_memtime() - d_t1;
+#endif
+                if (lh) {
                         m.hit = true;
                         m.node = node;
                         break;
                 }
         }
+#if VRT_PHASE_STAMPS
+        {
+                // every lane has left the loop: wave-level totals
+                const uint32_t itmax = wave_max_u32(d_it), itsum = wave_sum_u32(d_it);
+                const uint32_t lpmax = wave_max_u32(d_lp), lpsum = wave_sum_u32(d_lp);
+                const uint32_t trimax = wave_max_u32(d_tri), trisum = wave_sum_u32(d_tri);
+                // the stamps are per lane but the loop ran as one wave: the
+                // lane with the longest walk saw all of it
+                unsigned long long tin = d_tin, tleaf = d_tleaf;
+                for (int o = 32; o > 0; o >>= 1) {
+                        tin = max(tin, (unsigned long long)__shfl_xor((long long)tin, o, 64));
+                        tleaf = max(tleaf, (unsigned long long)__shfl_xor((long long)tleaf, o, 64));
+                }
+                // wave-uniform sums kept by every lane while it walked: the
+                // lane that walked longest holds the full totals
+                const uint32_t lpm = wave_max_u32(d_phmax);
+                const uint32_t lps = wave_max_u32(d_lpsum);
+                if ((threadIdx.x & 63) == 0) {
+                        atomicAdd(&g_phase[0], (unsigned long long)itmax);
+                        atomicAdd(&g_phase[1], (unsigned long long)itsum);
+                        atomicAdd(&g_phase[2], (unsigned long long)lpmax);
+                        atomicAdd(&g_phase[3], (unsigned long long)lpsum);
+                        atomicAdd(&g_phase[4], (unsigned long long)trimax);
+                        atomicAdd(&g_phase[5], (unsigned long long)trisum);
+                        atomicAdd(&g_phase[6], (unsigned long long)lpm);
+                        atomicAdd(&g_phase[7], (unsigned long long)lps);
+                        atomicAdd(&g_phase[8], tin);
+                        atomicAdd(&g_phase[9], tleaf);
+                        atomicAdd(&g_phase[11], 1ull);
+                }
+        }
+#endif
 #else
         for (;;) {
                 if (cnt == 0) {
@@ -795,18 +901,26 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
 #endif
         if (__all(sc.fast_ok && fast_ok(r))) {
                 if (VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
-                        ray_march<kCount, true, kS, true, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, 1, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
                 else
-                        ray_march<kCount, true, kS, false, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, 0, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
         } else
-                ray_march<kCount, false, kS, false, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
+                ray_march<kCount, false, kS, 0, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
 }
 
 // True when ray_march's fast, standard-range instantiation is exact for
-// every lane of the wave (the first branch of ray_march_dispatch).
+// every lane of the wave (the first branch of ray_march_dispatch); with
+// VRT_FIN also every |dinv| <= 2^64 (expand_v2<2>'s finite slab distances).
+#ifndef VRT_FIN
+#define VRT_FIN 1
+#endif
+constexpr int kFastStd = VRT_FIN ? 2 : 1;
 __device__ __forceinline__ bool wave_fast_std(const DevScene &sc, const RayK &r)
 {
-        return __all(sc.fast_ok && fast_ok(r) && __float_as_uint(r.tmin) == 0u && r.tmax == kFltMax);
+        bool ok = sc.fast_ok && fast_ok(r) && __float_as_uint(r.tmin) == 0u && r.tmax == kFltMax;
+        if (VRT_FIN)
+                ok = ok && fabsf(r.dinv.x) <= 0x1p64f && fabsf(r.dinv.y) <= 0x1p64f && fabsf(r.dinv.z) <= 0x1p64f;
+        return __all(ok);
 }
 
 // ---------------------------------------------------------------------------
@@ -1111,7 +1225,7 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         if (kFastOnly) {
                 if (!wave_fast_std(p.sc, r) || (p.test_flags & VRT_TEST_FORCE_DEFER))
                         return false;
-                ray_march<false, true, kS, true, true, kR64, kNS>(p.sc, r, stk, nullptr, nullptr, m);
+                ray_march<false, true, kS, kFastStd, true, kR64, kNS>(p.sc, r, stk, nullptr, nullptr, m);
         } else {
                 ray_march_dispatch<kCount, kS, true, kR64, kNS>(p.sc, r, stk, stk_aux, path_rem, m);
         }
@@ -1260,9 +1374,16 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
                         if (u >= (uint32_t)(hi - lo))
                                 break;
                         const int kq = unit_tile_sub(um, x, lo + (int)u, lo);
-                        if (!render_unit<false, false, kPersistBlock, false, kFastOnly, kNS>(
-                                    p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr) &&
-                            lane == 0) {
+#if VRT_PHASE_STAMPS
+                        const unsigned long long d_u0 = __builtin_amdgcn_s_memtime();
+#endif
+                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kNS>(
+                                p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr);
+#if VRT_PHASE_STAMPS
+                        if (lane == 0)
+                                atomicAdd(&g_phase[10], __builtin_amdgcn_s_memtime() - d_u0);
+#endif
+                        if (!done && lane == 0) {
                                 const uint32_t d = atomicAdd(p.q.defer, 1u);
                                 if (d < (uint32_t)kDeferCap)
                                         p.q.defer[kDeferList + d] = (uint32_t)kq;
@@ -2573,3 +2694,17 @@ hipError_t launch_iota(uint32_t *v, int64_t n, hipStream_t st)
 }
 
 }  // namespace vrt
+
+#if VRT_PHASE_STAMPS
+extern "C" __attribute__((visibility("default"))) int vrt_diag_phases(unsigned long long out[16], int reset)
+{
+        if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_phase), sizeof(unsigned long long) * 16) != hipSuccess)
+                return -1;
+        if (reset) {
+                unsigned long long z[16] = {};
+                if (hipMemcpyToSymbol(HIP_SYMBOL(vrt::g_phase), z, sizeof z) != hipSuccess)
+                        return -1;
+        }
+        return 0;
+}
+#endif
