@@ -1205,19 +1205,28 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         // the lane id is re-read per unit (volatile asm: not hoisted out of
         // a persistent loop), so its derived per-lane constants are
         // recomputed instead of being held -- and spilled -- across units
-        if (!kSamples)
-                asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        auto lane_now = [&]() {
+                int l = lane;
+                if (!kSamples)
+                        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+                return l;
+        };
+        const CamParams &c = p.cam;
         const int t = p.rank + k * p.nranks;
         const int tx = t % p.ntx, ty = t / p.ntx;
-        const int s = lane & 3, pix = lane >> 2;
-        const int lx = (wave & 1) * 4 + (pix & 3);
-        const int ly = (wave >> 1) * 4 + (pix >> 2);
-        const int px = tx * 8 + lx, py = ty * 8 + ly;
-        const CamParams &c = p.cam;
-
-        // Camera::gen_rays4 (VRT/camera.cc:95-112)
-        const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
-                                 sample_x(s), sample_y(s));
+        // pixel, sample and Camera::gen_rays4 direction (VRT/camera.cc:95-112)
+        // of lane l
+        auto sample_of = [&](int l, int &px, int &py, int &s, int &lx, int &ly) {
+                s = l & 3;
+                const int pix = l >> 2;
+                lx = (wave & 1) * 4 + (pix & 3);
+                ly = (wave >> 1) * 4 + (pix >> 2);
+                px = tx * 8 + lx;
+                py = ty * 8 + ly;
+                return camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py, sample_x(s), sample_y(s));
+        };
+        int px, py, s, lx, ly;
+        f3 dn = sample_of(lane_now(), px, py, s, lx, ly);
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
 
@@ -1229,14 +1238,28 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         } else {
                 ray_march_dispatch<kCount, kS, true, kR64, kNS>(p.sc, r, stk, stk_aux, path_rem, m);
         }
+        // persistent kernels: the pixel (and with VRT_REDIR the direction)
+        // are made again -- the same operations, so the same bits -- rather
+        // than held live across the march
+#ifndef VRT_REDIR
+#define VRT_REDIR 0
+#endif
+        if (!kSamples) {
+                const f3 d2 = sample_of(lane_now(), px, py, s, lx, ly);
+                if (VRT_REDIR)
+                        dn = d2;
+        }
 
         f3 col;
         if (m.hit) {
                 f3 nrm;
-                col = shade_hit(p.sc, r, m, nrm);
+                RayK rs;  // shade_hit reads the direction only
+                rs.d = dn;
+                col = shade_hit(p.sc, rs, m, nrm);
         } else {
-                col = sky(r.d.y);
+                col = sky(dn.y);
         }
+        lane = lane_now();
 
         const size_t si = ((size_t)py * c.nx + px) * 4 + s;
         if (kSamples) {
