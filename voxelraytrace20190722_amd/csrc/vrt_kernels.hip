@@ -939,7 +939,11 @@ __device__ __forceinline__ bool wave_fast_std(const DevScene &sc, const RayK &r)
 
 // The 8 children's slab tests (kFast: expand_v2's planes and v_max3/v_min3;
 // otherwise expand_v1's exact select semantics) -> hit mask, bit ci.
-template <bool kFast>
+// kFin (with kFast; the wave's rays have tmax == FLT_MAX, a tmin that is not
+// NaN and every |dinv| <= 2^64, so every slab distance is finite): the
+// reference's range test !(t0 > t1) && (t0 in [tmin, tmax] || t1 in [tmin,
+// tmax]) is exactly max(t0, tmin) <= t1 (as expand_v2<2> with tmin = +0).
+template <bool kFast, bool kFin = false>
 __device__ __forceinline__ uint32_t child_hit_mask(const float bmin[3], const float bmax[3], const RayK &r)
 {
         const float oo[3] = { r.o.x, r.o.y, r.o.z };
@@ -968,6 +972,10 @@ __device__ __forceinline__ uint32_t child_hit_mask(const float bmin[3], const fl
                         fr[k][1] = std_max(tb1, tc);
                 }
         }
+        if (kFin) {
+                nr[2][0] = fmaxf(nr[2][0], r.tmin);
+                nr[2][1] = fmaxf(nr[2][1], r.tmin);
+        }
         uint32_t hm = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -976,6 +984,10 @@ __device__ __forceinline__ uint32_t child_hit_mask(const float bmin[3], const fl
                 if (kFast) {
                         asm("v_max3_f32 %0, %1, %2, %3" : "=v"(t0) : "v"(nr[0][mx]), "v"(nr[1][my]), "v"(nr[2][mz]));
                         asm("v_min3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(fr[0][mx]), "v"(fr[1][my]), "v"(fr[2][mz]));
+                        if (kFin) {
+                                hm |= (uint32_t)(t0 <= t1) << i;  // t0 = max(near distances, tmin)
+                                continue;
+                        }
                 } else {
                         t0 = nr[0][mx];
                         t1 = fr[0][mx];
@@ -1052,7 +1064,7 @@ __device__ __forceinline__ bool leaf_any(const void *__restrict__ refs, uint32_t
         return false;
 }
 
-template <bool kFast, int kS, bool kR64>
+template <bool kFast, int kS, bool kR64, bool kFin = false>
 __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, uint2 *stk)
 {
         float bmin[3], bmax[3];
@@ -1064,7 +1076,7 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
                 return leaf_any<kR64>(sc.refs, b, a & ~kLeafBit, r);
         // children in ascending (ci ^ s): the near half of each axis first
         const uint32_t s = (r.d.x < 0.f ? 4u : 0u) | (r.d.y < 0.f ? 2u : 0u) | (r.d.z < 0.f ? 1u : 0u);
-        uint32_t mask = xor_permute8(child_hit_mask<kFast>(bmin, bmax, r) & b, s);
+        uint32_t mask = xor_permute8(child_hit_mask<kFast, kFin>(bmin, bmax, r) & b, s);
         uint32_t base = a;
         int sp = 0;
         for (;;) {
@@ -1089,7 +1101,7 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
                                         stk[sp * kS] = make_uint2(base, mask);
                                         ++sp;
                                 }
-                                mask = xor_permute8(child_hit_mask<kFast>(bmin, bmax, r) & b, s);
+                                mask = xor_permute8(child_hit_mask<kFast, kFin>(bmin, bmax, r) & b, s);
                                 base = a;
                                 continue;
                         }
@@ -1122,8 +1134,15 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
 template <int kS, bool kR64>
 __device__ __forceinline__ bool ray_occluded_dispatch(const DevScene &sc, const RayK &r, uint2 *stk)
 {
-        if (__all(sc.fast_ok && fast_ok(r)))
-                return ray_occluded<true, kS, kR64>(sc, r, stk);
+        // VRT_FIN: the fast walk is the finite-distance one (child_hit_mask's
+        // kFin); a wave with a ray outside it (a tiny or zero direction
+        // component, tmax != FLT_MAX, a NaN tmin) takes the exact walk
+        bool ok = sc.fast_ok && fast_ok(r);
+        if (VRT_FIN)
+                ok = ok && r.tmax == kFltMax && !isnan(r.tmin) && fabsf(r.dinv.x) <= 0x1p64f &&
+                     fabsf(r.dinv.y) <= 0x1p64f && fabsf(r.dinv.z) <= 0x1p64f;
+        if (__all(ok))
+                return ray_occluded<true, kS, kR64, VRT_FIN != 0>(sc, r, stk);
         return ray_occluded<false, kS, kR64>(sc, r, stk);
 }
 
