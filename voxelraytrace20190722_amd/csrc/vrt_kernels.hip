@@ -386,13 +386,14 @@ __device__ __forceinline__ uint32_t expand_v1(const float bmin[3],
 // kStd >= 1: every lane's ray has tmin == +0 and tmax == FLT_MAX, so (fast
 // path, no NaN) `t >= tmin && t <= tmax` is exactly "t is +-0, +subnormal or
 // +normal" -- one v_cmp_class instead of two compares and an AND.
-// kStd == 2: in addition every |dinv| <= 2^64 (no zero or tiny direction
-// component), so with |plane - o| < 2^61 (fast_ok) every slab distance is
-// finite and the reference's test !(t0 > t1) && (t0 in [0, FLT_MAX] ||
-// t1 in [0, FLT_MAX]) is exactly t0 <= t1 && t1 >= 0 (the second clause
-// follows from t1 >= 0 when t0 <= t1, and neither endpoint can be +inf),
-// i.e. max(t0, 0) <= t1: the 0 is folded into one axis's near distances
-// once per expansion, leaving max3, min3 and one compare per child.
+// kStd == 2 (instead of the above): tmax == FLT_MAX, tmin is not NaN and
+// every |dinv| <= 2^64 (no zero or tiny direction component), so with
+// |plane - o| < 2^61 (fast_ok) every slab distance is finite and the
+// reference's test !(t0 > t1) && (t0 in [tmin, FLT_MAX] || t1 in [tmin,
+// FLT_MAX]) is exactly t0 <= t1 && t1 >= tmin (the second clause follows
+// from t1 >= tmin when t0 <= t1, and neither endpoint can be +inf), i.e.
+// max(t0, tmin) <= t1: tmin is folded into one axis's near distances once
+// per expansion, leaving max3, min3 and one compare per child.
 template <int kStd>
 __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float bmax[3], const RayK &r, int &cnt,
                                               uint32_t content)
@@ -422,8 +423,8 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
                 fr[k][1] = fmaxf(tb, tc);
         }
         if (kStd == 2) {
-                nr[2][0] = fmaxf(nr[2][0], 0.0f);
-                nr[2][1] = fmaxf(nr[2][1], 0.0f);
+                nr[2][0] = fmaxf(nr[2][0], r.tmin);
+                nr[2][1] = fmaxf(nr[2][1], r.tmin);
         }
         uint32_t hm = 0;
 #pragma unroll
@@ -891,6 +892,17 @@ __device__ __forceinline__ bool fast_ok(const RayK &r)
         return ok;
 }
 
+// expand_v2<2> / child_hit_mask<.., true> preconditions beyond fast_ok():
+// tmax = FLT_MAX, tmin not NaN, every |dinv| <= 2^64 (finite slab distances)
+#ifndef VRT_FIN
+#define VRT_FIN 1
+#endif
+__device__ __forceinline__ bool fin_ok(const RayK &r)
+{
+        return r.tmax == kFltMax && !isnan(r.tmin) && fabsf(r.dinv.x) <= 0x1p64f && fabsf(r.dinv.y) <= 0x1p64f &&
+               fabsf(r.dinv.z) <= 0x1p64f;
+}
+
 template <bool kCount, int kS, bool kUni, bool kR64, int kNS = 0>
 __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const RayK &r,
                                                    uint2 *sb, uint32_t *sa, uint32_t *pr,
@@ -900,7 +912,9 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
 #define VRT_STD_RANGE 1
 #endif
         if (__all(sc.fast_ok && fast_ok(r))) {
-                if (VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
+                if (VRT_FIN && !kCount && __all(fin_ok(r)))
+                        ray_march<kCount, true, kS, 2, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
+                else if (!VRT_FIN && VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
                         ray_march<kCount, true, kS, 1, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
                 else
                         ray_march<kCount, true, kS, 0, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
@@ -908,18 +922,15 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
                 ray_march<kCount, false, kS, 0, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
 }
 
-// True when ray_march's fast, standard-range instantiation is exact for
-// every lane of the wave (the first branch of ray_march_dispatch); with
-// VRT_FIN also every |dinv| <= 2^64 (expand_v2<2>'s finite slab distances).
-#ifndef VRT_FIN
-#define VRT_FIN 1
-#endif
+// True when ray_march's fast instantiation for camera rays is exact for
+// every lane of the wave: standard range (tmin = +0, tmax = FLT_MAX) and,
+// with VRT_FIN, finite slab distances (fin_ok).
 constexpr int kFastStd = VRT_FIN ? 2 : 1;
 __device__ __forceinline__ bool wave_fast_std(const DevScene &sc, const RayK &r)
 {
         bool ok = sc.fast_ok && fast_ok(r) && __float_as_uint(r.tmin) == 0u && r.tmax == kFltMax;
         if (VRT_FIN)
-                ok = ok && fabsf(r.dinv.x) <= 0x1p64f && fabsf(r.dinv.y) <= 0x1p64f && fabsf(r.dinv.z) <= 0x1p64f;
+                ok = ok && fin_ok(r);
         return __all(ok);
 }
 
@@ -1139,8 +1150,7 @@ __device__ __forceinline__ bool ray_occluded_dispatch(const DevScene &sc, const 
         // component, tmax != FLT_MAX, a NaN tmin) takes the exact walk
         bool ok = sc.fast_ok && fast_ok(r);
         if (VRT_FIN)
-                ok = ok && r.tmax == kFltMax && !isnan(r.tmin) && fabsf(r.dinv.x) <= 0x1p64f &&
-                     fabsf(r.dinv.y) <= 0x1p64f && fabsf(r.dinv.z) <= 0x1p64f;
+                ok = ok && fin_ok(r);
         if (__all(ok))
                 return ray_occluded<true, kS, kR64, VRT_FIN != 0>(sc, r, stk);
         return ray_occluded<false, kS, kR64>(sc, r, stk);
