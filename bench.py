@@ -526,7 +526,8 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle as po
         osc = po.Scene(sd, a.depth)
-        nth = max(1, min(a.cpu_threads, os.cpu_count() or 1))
+        ci = cpu_info()
+        nth = max(1, min(a.cpu_threads or ci["nproc"], 64))  # as the primary baseline below
         t0_ = time.perf_counter()
         osc.lightmap(po.camera(vrt.to_radian(60), (1, 10, 1), (0, 0, 0), (0, 1, 0)), 1.0, 1.0, a.light_n,
                      a.light_n, nthreads=nth)
@@ -539,6 +540,7 @@ def main():
         t2_ = time.perf_counter()
         tr = (t2_ - t1_) * (a.width * a.height) / (hw * hh)
         cpu = {"value": round(1.0 / ((t1_ - t0_) + tr), 5), "unit": "frames/s", "cores": nth, "kind": "port",
+               "nproc": ci["nproc"], "cgroup_quota_cpus": ci["cgroup_quota_cpus"], "cpu_model": ci["model"],
                "sample": f"light map {a.light_n}^2 x4 + filter ({t1_ - t0_:.1f} s) + cone-traced {hw}x{hh} x4 "
                          f"({t2_ - t1_:.1f} s, scaled x{(a.width * a.height) / (hw * hh):.0f} to "
                          f"{a.width}x{a.height}) by oracle/vrt_oracle.c over {nth} threads"}
