@@ -17,7 +17,7 @@ HIPFLAGS := -x hip --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 $(FP) -Iinclude -
 CXXFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Wall -fvisibility=hidden
 
 HOSTOBJS := $(BLD)/vrt_host.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o
-OBJS := $(BLD)/vrt_kernels.o $(BLD)/vrt_sort.o $(BLD)/vrt_build.o $(HOSTOBJS) $(BLD)/vrt_build_id.o
+OBJS := $(BLD)/vrt_kernels.o $(BLD)/vrt_build.o $(HOSTOBJS) $(BLD)/vrt_build_id.o
 HDRS := include/vrt.h $(SRC)/vrt_math.h $(SRC)/vrt_internal.h $(SRC)/vrt_error.h
 
 all: $(PKG)/libvrt.so oracle
@@ -31,9 +31,6 @@ KFLAGS := -mllvm -amdgpu-atomic-optimizer-strategy=DPP
 
 $(BLD)/vrt_kernels.o: $(SRC)/vrt_kernels.hip $(HDRS) | $(BLD)
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -c $< -o $@
-
-$(BLD)/vrt_sort.o: $(SRC)/vrt_sort.hip $(HDRS) | $(BLD)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BLD)/vrt_build.o: $(SRC)/vrt_build.hip $(HDRS) | $(BLD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -70,19 +67,19 @@ oracle:
 	$(MAKE) -C oracle
 
 # A/B variant of the kernels:  make variant NAME=v0 DEFS="-DVRT_EXPAND_V=0"
-variant: $(HOSTOBJS) $(BLD)/vrt_sort.o $(BLD)/vrt_build.o | $(BLD)
+variant: $(HOSTOBJS) $(BLD)/vrt_build.o | $(BLD)
 	mkdir -p build/variants
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
-	  build/variants/k_$(NAME).o $(BLD)/vrt_sort.o $(BLD)/vrt_build.o $(HOSTOBJS) -lpthread
+	  build/variants/k_$(NAME).o $(BLD)/vrt_build.o $(HOSTOBJS) -lpthread
 
 # variant that also rebuilds the host side (for data-layout changes)
-fullvariant: $(BLD)/vrt_sort.o $(BLD)/vrt_build.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o | $(BLD)
+fullvariant: $(BLD)/vrt_build.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o | $(BLD)
 	mkdir -p build/variants
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_host.cpp -o build/variants/h_$(NAME).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
-	  build/variants/k_$(NAME).o build/variants/h_$(NAME).o $(BLD)/vrt_sort.o $(BLD)/vrt_build.o \
+	  build/variants/k_$(NAME).o build/variants/h_$(NAME).o $(BLD)/vrt_build.o \
 	  $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o -lpthread
 
 # ISA listing + register/occupancy report of the kernels (for DESIGN.md)

@@ -11,6 +11,7 @@ bash tools/gpu_steps.sh \
   "bench|400|python -u bench.py --pmc-save $R/gpurun_out/pmc_bench" \
   "bench_sec|400|python -u bench.py --mode secondary --pmc-save $R/gpurun_out/pmc_sec" \
   "bench_4k|400|python -u bench.py --width 3840 --height 2160 --depth 9 --no-d9 --pmc-save $R/gpurun_out/pmc_4k" \
+  "bench_trace|300|python -u bench.py --mode trace" \
   "trace_p|300|$TR -d $R/gpurun_out/trace_bench -o trace -- python3 $R/bench.py --no-cpu --no-pmc --no-counters --no-d9" \
   "trace_s|300|$TR -d $R/gpurun_out/trace_sec -o trace -- python3 $R/bench.py --mode secondary --no-cpu --no-pmc" \
   "gloo2|300|python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 8 --warmup 2 --dist-backend gloo"

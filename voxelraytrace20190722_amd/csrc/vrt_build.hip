@@ -451,4 +451,15 @@ hipError_t build_tree_device(int device, const float *pos, int ntri, const float
         return hipSuccess;
 }
 
+// Stable device radix sort of (uint32 key, uint32 value) pairs on the low
+// `bits` key bits, for the light-map accumulation (vrt_kernels.hip: leaf
+// key, canonical sample index); the same hipCUB / rocPRIM onesweep sort the
+// build's frontier uses, so hipCUB's templates compile in this one file.
+hipError_t sort_pairs_u32(void *temp, size_t *temp_bytes, const uint32_t *keys_in, uint32_t *keys_out,
+                          const uint32_t *vals_in, uint32_t *vals_out, int64_t n, int bits, hipStream_t st)
+{
+        return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out,
+                                                  (int)n, 0, bits, st);
+}
+
 }  // namespace vrt

@@ -301,7 +301,7 @@ hipError_t launch_trace(const TraceParams &p, hipStream_t st);
 hipError_t launch_lm_aux(const NodeRec *nodes, const LMRec *lm, int64_t n, float4 *cc, uint32_t *bad,
                          hipStream_t st);
 // stable radix sort of (key, value) pairs on the low `bits` key bits
-// (vrt_sort.hip); temp == nullptr queries *temp_bytes
+// (vrt_build.hip); temp == nullptr queries *temp_bytes
 hipError_t sort_pairs_u32(void *temp, size_t *temp_bytes, const uint32_t *keys_in, uint32_t *keys_out,
                           const uint32_t *vals_in, uint32_t *vals_out, int64_t n, int bits, hipStream_t st);
 hipError_t launch_iota(uint32_t *v, int64_t n, hipStream_t st);
