@@ -693,6 +693,9 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
 #if VRT_PHASE_STAMPS
                 const unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
 #endif
+#ifndef VRT_POP_VISIT
+#define VRT_POP_VISIT 1
+#endif
                 for (;;) {
 #if VRT_PHASE_STAMPS
                         ++d_it;
@@ -711,7 +714,11 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                         fpos = x & 0xFFFFFFu;
                                         depth = x >> 24;
                                 }
-                                continue;
+                                // VRT_POP_VISIT: a pushed entry always has
+                                // cnt > 0, so the popped level's next child is
+                                // visited in this same iteration
+                                if (!VRT_POP_VISIT)
+                                        continue;
                         }
                         const uint32_t ci = order & 7u;
                         order >>= 3;
@@ -1102,7 +1109,8 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
                                 const uint2 e = stk[sp * kS];
                                 base = e.x;
                                 mask = e.y;
-                                continue;
+                                if (!VRT_POP_VISIT)  // pushed masks are non-zero: visit now
+                                        continue;
                         }
                         const uint32_t ci = (uint32_t)__builtin_ctz(mask) ^ s;
                         mask &= mask - 1u;
