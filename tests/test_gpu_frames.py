@@ -183,6 +183,24 @@ def test_forced_defer_pass_matches_oracle(proxy):
         assert np.array_equal(bits(got), bits(want))
 
 
+@pytest.mark.parametrize("near,far", [(0.05, vrt.FLT_MAX), (0.0, 2.5), (-1.0, 1e30)])
+def test_general_persistent_kernel_nonstandard_range_matches_oracle(proxy, near, far):
+    """A camera with near != +0 or far != FLT_MAX makes rays outside the
+    fast kernel's standard range: the production launch is then the general
+    persistent kernel (k_render_p<false>, render_kind), whose images must
+    equal the oracle's too (Camera's near / far are the rays' tmin / tmax,
+    VRT/camera.cc:65-75)."""
+    tree, osc = scenes(proxy, 8)
+    mn, mx = tree.root_box
+    p = vrt.sweep_pose(mn, mx, 6, 16)
+    cam = vrt.Camera(*p, near, far)
+    want = osc.render(po.camera(*p, near, far), 1.0, 1.0, 400, 240, nthreads=NTH, samples=False)
+    got = _device_image(tree, cam, vrt.Film(1, 1, 400, 240))
+    assert np.array_equal(bits(got), bits(want))
+    rgb, so = tree.render(cam, vrt.Film(1, 1, 400, 240), samples=True)  # the grid kernel (per-sample outputs)
+    assert np.array_equal(bits(rgb), bits(want))
+
+
 def _pack(seq):
     w = 0
     for k, c in enumerate(seq):
