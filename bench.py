@@ -251,6 +251,11 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (RCCL over xGMI, the real path) or gloo (host-staged rehearsal)")
     p.add_argument("--save-image", default="", help="rank 0 writes the last frame as .hdr")
+    p.add_argument("--rehearse-ranks", type=int, default=0,
+                   help="single-GPU rehearsal of the N-rank path (WORLD_SIZE 1): render rank 0's share of the "
+                        "tiles as one of R ranks, RCCL gather over a 1-rank process group, unpack of R rank "
+                        "buffers -- the per-rank GPU and host cost of the multi-GPU step without the xGMI "
+                        "transfer (reported as 'rehearsal', never as the N-GPU value)")
     a = p.parse_args()
     trace = a.mode == "trace"
     a.width = a.width or (1024 if trace else 1920)
@@ -269,11 +274,18 @@ def main():
     local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    rehearse = world == 1 and a.rehearse_ranks > 1 and a.mode == "primary"
     if world > 1:
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    elif rehearse:
+        # a 1-rank RCCL group: the gather below runs through RCCL exactly as
+        # in the N-rank step (its payload stays on this GPU)
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    # the number of tile shares the frame is dealt into
+    nshare = a.rehearse_ranks if rehearse else world
 
     # ---- scene: built on the host, uploaded once (excluded from timing)
     t0 = time.time()
@@ -314,7 +326,7 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
-    tpr = vrt.tiles_per_rank(film, world)
+    tpr = vrt.tiles_per_rank(film, nshare)
     secondary = a.mode == "secondary"
     img = torch.zeros((a.height, a.width) if secondary else (a.height, a.width, 3), dtype=torch.float32,
                       device=dev)
@@ -326,13 +338,14 @@ def main():
             _, frame_rays[pi] = tree.render_secondary(cams[pi], film, spp=a.spp)
         prim = torch.zeros(W8 * H8 * 8, dtype=torch.float32, device=dev)
         visb = [torch.zeros((a.height, a.width), dtype=torch.float32, device=dev) for _ in range(2)]
-    elif world > 1:
+    elif nshare > 1:
         # double-buffered: the RCCL gather of frame k (on the NCCL stream)
         # overlaps the render of frame k+1 (on the compute stream)
         tiles = [torch.zeros(tpr * 192, dtype=torch.float32, device=dev) for _ in range(2)]
-        gathered = ([torch.zeros((world, tpr * 192), dtype=torch.float32, device=dev) for _ in range(2)]
+        gathered = ([torch.zeros((nshare, tpr * 192), dtype=torch.float32, device=dev) for _ in range(2)]
                     if rank == 0 else None)
-        gl = [list(g.unbind(0)) for g in gathered] if rank == 0 else [None, None]  # in-place views
+        # in-place views (a rehearsal's 1-rank group gathers into row 0 only)
+        gl = [list(g[:world].unbind(0)) for g in gathered] if rank == 0 else [None, None]
     works = [None, None]
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(a.steps)]
@@ -347,7 +360,7 @@ def main():
             if secondary:
                 img.copy_(visb[b])
             else:
-                vrt.unpack_tiles_device(film, world, gathered[b].data_ptr(), img.data_ptr(), sp)
+                vrt.unpack_tiles_device(film, nshare, gathered[b].data_ptr(), img.data_ptr(), sp)
 
     def step_secondary(k, timed):
         cam = cams[k % a.poses]
@@ -396,14 +409,14 @@ def main():
                 light_ms.append((time.perf_counter() - t0_) * 1e3)
         if timed:
             ev[k][0].record(stream)
-        if world == 1:
+        if nshare == 1:
             render(cam, 0, 1, 1, img.data_ptr())
             if timed:
                 ev[k][1].record(stream)
             return
         b = k & 1
         finish(b)  # frame k-2 used this buffer pair
-        render(cam, rank, world, 0, tiles[b].data_ptr())
+        render(cam, rank, nshare, 0, tiles[b].data_ptr())
         if timed:
             ev[k][1].record(stream)
         finish(1 - b)  # frame k-1: its gather overlapped this render
@@ -449,7 +462,7 @@ def main():
     # convention): the same sweep timed on a second octree, reported in the
     # same line (N=1 primary bench only)
     d9 = None
-    if world == 1 and not secondary and not trace and not a.no_d9:
+    if world == 1 and not rehearse and not secondary and not trace and not a.no_d9:
         tree9 = vrt.VoxelOctree(sd, a.depth + 1, device=local)
         img9 = torch.zeros_like(img)
         for k in range(a.warmup):
@@ -478,7 +491,7 @@ def main():
     # the host-buffer entry point (vrt_render: device image -> host array
     # over PCIe, per call); reported next to the HBM-resident value, never as it
     host_out = None
-    if world == 1 and not secondary and not trace and not a.no_d9:
+    if world == 1 and not rehearse and not secondary and not trace and not a.no_d9:
         n_h = min(a.steps, 16)
         tree.render(cams[0], film)  # warm-up
         th = time.perf_counter()
@@ -492,7 +505,7 @@ def main():
 
     roof = None
     ref_bytes, per_ray = None, None
-    if not a.no_counters and not secondary and not trace:
+    if not a.no_counters and not rehearse and not secondary and not trace:
         poses_used = sorted({k % a.poses for k in range(a.steps)})
         b_rank = []
         cnt_tot = np.zeros(4)
@@ -519,7 +532,7 @@ def main():
         nr = cnt_tot / (len(poses_used) * rays_per_frame / world)
         per_ray = {"A": round(float(nr[0]), 2), "L": round(float(nr[1]), 2),
                    "T": round(float(nr[2]), 2), "H": round(float(nr[3]), 3)}
-    if rank == 0 and world == 1 and not trace and not a.no_pmc:
+    if rank == 0 and world == 1 and not rehearse and not trace and not a.no_pmc:
         pmc, why = run_pmc(a, "k_secondary" if secondary else "k_render", a.pmc_save)
         out_bytes = (W8 * H8 * 4) if secondary else (W8 * H8 * 12)
         if pmc:
@@ -560,7 +573,7 @@ def main():
                          f"({t2_ - t1_:.1f} s, scaled x{(a.width * a.height) / (hw * hh):.0f} to "
                          f"{a.width}x{a.height}) by oracle/vrt_oracle.c over {nth} threads"}
         osc.close()
-    if rank == 0 and world == 1 and not a.no_cpu and not secondary and not trace:
+    if rank == 0 and world == 1 and not rehearse and not a.no_cpu and not secondary and not trace:
         # The reference's scheduler: thread_pool_cpp with hardware_concurrency
         # workers (thread_pool_options.hpp:50-54) takes render_mt's 64 tile
         # tasks (VRT/camera.h:42-68), so min(nproc, 64) threads are ever
@@ -670,9 +683,23 @@ def main():
             out["depth_plus1"] = d9
         if host_out:
             out["host_output"] = host_out
+        if rehearse:
+            # not an N-GPU measurement: one rank's share of every frame plus
+            # the RCCL call sequence, on one GPU; the xGMI transfer is absent
+            out["metric"] = "rehearsal: " + metric
+            out["value"] = None
+            out["config"]["parallelism"] = f"rank 0 of {nshare} screen-tile shares + rccl gather (1-rank group)"
+            out["rehearsal"] = {
+                "ranks": nshare, "frames_per_s": round(a.steps / elapsed, 2),
+                "projected_Mrays_per_s_without_xgmi": round(value, 2),
+                "share_kernel_ms_mean": round(float(kms.mean()), 4),
+                "note": "per-rank step time of the N-rank path (render of 1/N of the tiles, RCCL gather, unpack "
+                        "of N rank buffers, Python host loop) on one GPU; a real N-GPU step adds the xGMI "
+                        "transfer into rank 0"}
+            out["kernel_mrays_per_s"] = round(mean_rays / nshare / (kms.mean() * 1e-3) / 1e6, 2)
         out["build_id"] = vrt.build_id()
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 or rehearse:
         dist.destroy_process_group()
 
 
