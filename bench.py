@@ -63,6 +63,8 @@ def workload_args(a):
            "--detail", str(a.detail), "--poses", str(a.poses), "--mode", a.mode, "--spp", str(a.spp)]
     if a.scene:
         out += ["--scene", a.scene]
+    if a.rehearse_ranks > 1:
+        out += ["--rehearse-ranks", str(a.rehearse_ranks)]
     return out
 
 
@@ -218,6 +220,13 @@ def cpu_info():
     return {"nproc": n, "affinity": aff, "cgroup_quota_cpus": quota, "model": model}
 
 
+def nccl_options():
+    try:
+        return dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
+    except Exception:  # noqa: BLE001 -- an older torch: default streams
+        return None
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -277,13 +286,16 @@ def main():
     rehearse = world == 1 and a.rehearse_ranks > 1 and a.mode == "primary"
     if world > 1:
         if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            # the collectives' stream at high priority: their kernels are
+            # dispatched ahead of the next render's persistent workgroups
+            dist.init_process_group("nccl", device_id=dev, pg_options=nccl_options())
         else:
             dist.init_process_group("gloo")
     elif rehearse:
         # a 1-rank RCCL group: the gather below runs through RCCL exactly as
         # in the N-rank step (its payload stays on this GPU)
-        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev,
+                                pg_options=nccl_options())
     # the number of tile shares the frame is dealt into
     nshare = a.rehearse_ranks if rehearse else world
 
@@ -380,9 +392,9 @@ def main():
         tree.render_secondary_device(cam, film, a.spp, rank, world, prim.data_ptr(), visb[b].data_ptr(), sp)
         if timed:
             ev[k][1].record(stream)
-        finish(1 - b)
         if a.dist_backend == "nccl":
             works[b] = dist.reduce(visb[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
+            finish(1 - b)
         else:
             host = visb[b].cpu()
             dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
@@ -415,13 +427,16 @@ def main():
                 ev[k][1].record(stream)
             return
         b = k & 1
-        finish(b)  # frame k-2 used this buffer pair
+        finish(b)  # frame k-2 used this buffer pair (normally finished already)
         render(cam, rank, nshare, 0, tiles[b].data_ptr())
         if timed:
             ev[k][1].record(stream)
-        finish(1 - b)  # frame k-1: its gather overlapped this render
         if a.dist_backend == "nccl":
+            # frame k's gather is queued as soon as its render is: the NCCL
+            # stream waits for this render only, so its kernel is ready before
+            # render k+1 (queued after frame k-1's unpack) and runs beside it
             works[b] = dist.gather(tiles[b], gl[b], dst=0, async_op=True)
+            finish(1 - b)  # frame k-1: its gather overlapped this render
         else:  # gloo rehearsal (several ranks on one GPU): host-staged gather
             host = tiles[b].cpu()
             hl = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
@@ -532,9 +547,9 @@ def main():
         nr = cnt_tot / (len(poses_used) * rays_per_frame / world)
         per_ray = {"A": round(float(nr[0]), 2), "L": round(float(nr[1]), 2),
                    "T": round(float(nr[2]), 2), "H": round(float(nr[3]), 3)}
-    if rank == 0 and world == 1 and not rehearse and not trace and not a.no_pmc:
+    if rank == 0 and world == 1 and not trace and not a.no_pmc:
         pmc, why = run_pmc(a, "k_secondary" if secondary else "k_render", a.pmc_save)
-        out_bytes = (W8 * H8 * 4) if secondary else (W8 * H8 * 12)
+        out_bytes = (W8 * H8 * 4) if secondary else (W8 * H8 * 12 // nshare)
         if pmc:
             roof = roofline_from_pmc(pmc, float(kms.mean()), out_bytes, ref_bytes)
             if per_ray:

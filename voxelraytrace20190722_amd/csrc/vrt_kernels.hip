@@ -1405,6 +1405,12 @@ __device__ __forceinline__ uint32_t take_unit(uint32_t *ctr)
 // the launch's deferred list, which k_render_defer renders afterwards.
 // kNS > 0: the first kNS node records are staged in LDS (VRT_LDS_NODES).
 constexpr int kPersistBlock = 256;
+// Block slots (256 threads, 4 waves each) a persistent launch for one rank of
+// a multi-GPU frame leaves free, so the RCCL kernel moving the previous frame
+// finds CU room beside the persistent grid instead of waiting for it to
+// drain: 32 of ~1280 resident slots, a multiple of 8 (the XCD map needs a
+// grid of whole XCD rounds).
+constexpr int kCollectiveReserve = 32;
 #ifndef VRT_PERSIST_WAVES_PER_EU
 #define VRT_PERSIST_WAVES_PER_EU 5
 #endif
@@ -1791,7 +1797,8 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
         if (q && secondary_uses_queue(rp.sc) && waves <= INT_MAX) {
                 sp.units = (int32_t)waves;
                 sp.q = *q;
-                const int g = (int)std::min<int64_t>(rp.sc.sec_blocks, ((waves + 3) / 4 + 7) & ~7LL);
+                const int cap = nranks > 1 ? std::max(8, rp.sc.sec_blocks - kCollectiveReserve) : rp.sc.sec_blocks;
+                const int g = (int)std::min<int64_t>(cap, ((waves + 3) / 4 + 7) & ~7LL);
                 void (*kern)(SecondaryParams) = w ? (any ? k_secondary_p<true, true> : k_secondary_p<true, false>)
                                                   : (any ? k_secondary_p<false, true> : k_secondary_p<false, false>);
                 hipLaunchKernelGGL(kern, dim3(g), dim3(kSecPBlock), 0, st, sp);
@@ -2004,7 +2011,10 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 // one resident generation of 4-wave workgroups (<= one per
                 // 4 units, a multiple of 8 for the XCD map)
                 const int need = (p.tiles_this_rank + 7) & ~7;  // 4 units per tile, 4 waves per block
-                const int g = std::min(p.sc.persist_blocks, need);
+                // (kCollectiveReserve: room for the RCCL gather of the previous frame)
+                const int cap = p.nranks > 1 ? std::max(8, p.sc.persist_blocks - kCollectiveReserve)
+                                             : p.sc.persist_blocks;
+                const int g = std::min(cap, need);
                 if (kind == kRenderPersistFast) {
                         hipLaunchKernelGGL(k_render_p<true>, dim3(g), dim3(kPersistBlock), 0, st, p);
                         hipLaunchKernelGGL(k_render_defer, dim3(1), dim3(kPersistBlock), 0, st, p);
