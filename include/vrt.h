@@ -162,12 +162,24 @@ int vrt_render(vrt_scene *s, const vrt_camera *cam, const vrt_film *film,
 
 /* Device-resident variant (inputs/outputs in HBM, enqueued on `stream`, a
  * hipStream_t or NULL for the null stream; no host synchronisation).
- * Screen = 8x8-pixel tiles, row-major, t = 0..ntiles-1; this call renders
- * tiles t = rank + k*nranks (k = 0..) into d_out packed tile-major:
- * d_out[(k*64 + (y%8)*8 + x%8)*3 + c], sized vrt_tiles_per_rank()*192
- * floats.  rank=0, nranks=1 with image_layout=1 writes the nx*ny*3 image
- * directly instead. */
+ * Screen = the ntx x nty grid of 8x8-pixel tiles (ntx = nx/8, nty = ny/8).
+ * The tile deal (one rule for every multi-rank entry point): with
+ * G = vrt_tile_deal_block() (G = 1 when nranks == 1), the whole G x G blocks
+ * of tiles are dealt round-robin in block raster order (block j -> rank
+ * j % nranks); the tiles outside the whole-block region -- the right strip
+ * (rows ty < G*(nty/G), columns tx >= G*(ntx/G)), then the bottom strip, each
+ * in raster order -- continue the deal one tile at a time (leftover i ->
+ * rank (F + i) % nranks, F = number of whole blocks).  A rank's k-th tile:
+ * its blocks' tiles first (block order, row-major inside a block), then its
+ * leftover tiles.  This call renders this rank's tiles into d_out packed
+ * tile-major: d_out[(k*64 + (y%8)*8 + x%8)*3 + c], sized
+ * vrt_tiles_per_rank()*192 floats (the largest share).  rank=0, nranks=1
+ * with image_layout=1 writes the nx*ny*3 image directly instead. */
 int vrt_tiles_per_rank(const vrt_film *film, int nranks);
+int vrt_tile_deal_block(void);
+/* The deal as tables (host, no device): for every tile ty*ntx+tx, its rank
+ * and its index k in that rank's buffer. */
+int vrt_tile_deal_map(const vrt_film *film, int nranks, int32_t *rank_of_tile, int32_t *slot_of_tile);
 int vrt_render_tiles_device(vrt_scene *s, const vrt_camera *cam,
                             const vrt_film *film, int rank, int nranks,
                             int image_layout, float *d_out, void *stream);
@@ -194,8 +206,8 @@ int vrt_render_secondary(vrt_scene *s, const vrt_camera *cam,
                          const vrt_film *film, int spp, float *vis,
                          int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox,
                          int64_t *rays);
-/* Device-resident variant: rank `rank` of `nranks` writes its pixels (the
- * 8x8-pixel tiles t with t % nranks == rank) into d_vis (nx*ny floats, caller-zeroed:
+/* Device-resident variant: rank `rank` of `nranks` writes its pixels (its
+ * 8x8-pixel tiles of the tile deal, vrt_render_tiles_device) into d_vis (nx*ny floats, caller-zeroed:
  * a sum-reduce over ranks assembles the image exactly); d_prim = scratch of
  * 8*(nx/8)*8*(ny/8)*8 floats. */
 int vrt_render_secondary_device(vrt_scene *s, const vrt_camera *cam,

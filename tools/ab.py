@@ -43,6 +43,10 @@ def main():
     ap.add_argument("--mode", default="primary", choices=["primary", "secondary"])
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--no-check", action="store_true", help="timing-only variants (images may differ)")
+    ap.add_argument("--ranks", type=int, default=1,
+                    help="primary mode: time every rank's share of an N-rank frame separately (launch by launch; "
+                         "per pose the slowest rank counts, as in an N-GPU step), images re-assembled with each "
+                         "variant's own vrt_unpack_tiles_device for the parity check")
     a = ap.parse_args()
     sd = vrt.SceneData.proxy(a.detail, 1)
     film = _ffi.Film(1.0, 1.0, a.width, a.height)
@@ -69,12 +73,38 @@ def main():
     imgs = [torch.zeros((a.height, a.width) if sec else (a.height, a.width, 3), dtype=torch.float32, device=dev)
             for _ in libs]
     prim = torch.zeros(a.width * a.height * 8, dtype=torch.float32, device=dev)
+    R = a.ranks if not sec else 1
+    tprs = [L.vrt_tiles_per_rank(C.byref(film), R) for L in libs]
+    packs = [torch.zeros((R, tpr * 192), dtype=torch.float32, device=dev) for tpr in tprs]
     times = {p: [] for p in a.libs}
     ref = None
     for r in range(a.rounds + 1):
         for vi, (L, h, p) in enumerate(zip(libs, scenes, a.libs)):
             evs = []
             for ci, cam in enumerate(cams):
+                if R > 1:
+                    pe = []
+                    for rk in range(R):
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e0.record(st)
+                        rc = L.vrt_render_tiles_device(h, C.byref(cam), C.byref(film), rk, R, 0,
+                                                       C.c_void_p(packs[vi][rk].data_ptr()),
+                                                       C.c_void_p(st.cuda_stream))
+                        assert rc == 0, L.vrt_last_error()
+                        e1.record(st)
+                        pe.append((e0, e1))
+                    evs.append(pe)
+                    if r == 0 and ci == a.poses - 1:
+                        L.vrt_unpack_tiles_device(C.byref(film), R, C.c_void_p(packs[vi].data_ptr()),
+                                                  C.c_void_p(imgs[vi].data_ptr()), C.c_void_p(st.cuda_stream))
+                        torch.cuda.synchronize()
+                        im = imgs[vi].cpu().numpy().view(np.uint32)
+                        if ref is None:
+                            ref = im
+                        elif not a.no_check and not np.array_equal(im, ref):
+                            raise SystemExit(f"variant {p} differs from baseline {a.libs[0]}")
+                    continue
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(st)
@@ -97,7 +127,9 @@ def main():
                     elif not a.no_check and not np.array_equal(im, ref):
                         raise SystemExit(f"variant {p} differs from baseline {a.libs[0]}")
             torch.cuda.synchronize()
-            if r > 0:  # round 0 = warm-up + parity
+            if r > 0 and R > 1:  # per pose the slowest rank's launch
+                times[p].append(sum(max(s.elapsed_time(e) for s, e in pe) for pe in evs) / len(evs))
+            elif r > 0:  # round 0 = warm-up + parity
                 times[p].append(sum(s.elapsed_time(e) for s, e in evs) / len(evs))
     base = np.median(times[a.libs[0]])
     out = {}

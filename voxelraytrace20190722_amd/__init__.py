@@ -10,14 +10,14 @@ from .api import (  # noqa: F401
     FLT_MAX, Camera, Film, ObjModel, SceneData, VoxelOctree, build_id, device_count, device_selftest,
     device_selftest_order,
     hdr_bytes, hdr_bytes_from_rgbe, intersect_triangle3, load_image, make_ray, obj2voxel, ray_march, ray_march_init,
-    TEST_FORCE_DEFER, render, set_test_flags, sweep_pose, tga_decode, tiles_per_rank, to_radian, tri_box_overlap,
+    TEST_FORCE_DEFER, render, set_test_flags, sweep_pose, tga_decode, tile_deal_map, tiles_per_rank, to_radian, tri_box_overlap,
     unpack_tiles_device, write_hdr, rgbe_device, write_hdr_device,
 )
 
 __all__ = [
     "VrtError", "lib", "LIB_PATH", "FLT_MAX", "Camera", "Film", "SceneData", "VoxelOctree",
     "device_count", "device_selftest", "hdr_bytes", "intersect_triangle3", "make_ray",
-    "ray_march", "ray_march_init", "render", "sweep_pose", "tiles_per_rank", "to_radian",
+    "ray_march", "ray_march_init", "render", "sweep_pose", "tile_deal_map", "tiles_per_rank", "to_radian",
     "tri_box_overlap", "unpack_tiles_device", "write_hdr", "ObjModel", "obj2voxel", "load_image",
     "tga_decode", "hdr_bytes_from_rgbe", "rgbe_device", "write_hdr_device", "build_id", "device_selftest_order", "set_test_flags",
 ]

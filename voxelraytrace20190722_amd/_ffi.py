@@ -104,6 +104,8 @@ SIGNATURES = {
     "vrt_render": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), f32p,
                              C.POINTER(Samples), C.POINTER(Stats)]),
     "vrt_tiles_per_rank": (C.c_int, [C.POINTER(Film), C.c_int]),
+    "vrt_tile_deal_block": (C.c_int, []),
+    "vrt_tile_deal_map": (C.c_int, [C.POINTER(Film), C.c_int, i32p, i32p]),
     "vrt_render_tiles_device": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), C.c_int,
                                           C.c_int, C.c_int, _P, _P]),
     "vrt_unpack_tiles_device": (C.c_int, [C.POINTER(Film), C.c_int, _P, _P, _P]),

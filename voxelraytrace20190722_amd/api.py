@@ -465,6 +465,17 @@ def tiles_per_rank(film, nranks):
     return lib().vrt_tiles_per_rank(C.byref(film.c), int(nranks))
 
 
+def tile_deal_map(film, nranks):
+    """The library's tile deal as (nty, ntx) arrays: each tile's rank and its
+    index in that rank's packed buffer (vrt_tile_deal_map)."""
+    ntx, nty = film.nx // 8, film.ny // 8
+    rk = np.zeros((nty, ntx), np.int32)
+    sl = np.zeros((nty, ntx), np.int32)
+    check(lib().vrt_tile_deal_map(C.byref(film.c), int(nranks), ptr(rk, _ffi.i32p), ptr(sl, _ffi.i32p)),
+          "vrt_tile_deal_map")
+    return rk, sl
+
+
 def unpack_tiles_device(film, nranks, d_gathered_ptr, d_image_ptr, stream_ptr=None):
     check(lib().vrt_unpack_tiles_device(C.byref(film.c), int(nranks), C.c_void_p(d_gathered_ptr),
                                         C.c_void_p(d_image_ptr),

@@ -916,8 +916,41 @@ extern "C" int vrt_tiles_per_rank(const vrt_film *film, int nranks)
 {
         if (film_ok(film) || nranks < 1)
                 return 0;
-        const int T = (film->nx / 8) * (film->ny / 8);
-        return (T + nranks - 1) / nranks;
+        // the largest share of the tile deal (tile_deal, vrt_internal.h)
+        const TileDeal d = tile_deal(film->nx / 8, film->ny / 8, nranks);
+        int m = 0;
+        for (int r = 0; r < nranks; ++r)
+                m = std::max(m, deal_count(d, r));
+        return m;
+}
+
+extern "C" int vrt_tile_deal_block(void)
+{
+        return VRT_DEAL_BLOCK;
+}
+
+extern "C" int vrt_tile_deal_map(const vrt_film *film, int nranks, int32_t *rank_of_tile, int32_t *slot_of_tile)
+{
+        if (int rc = film_ok(film))
+                return rc;
+        if (nranks < 1 || !rank_of_tile || !slot_of_tile)
+                return fail(VRT_E_INVALID, "bad argument");
+        const int ntx = film->nx / 8, nty = film->ny / 8;
+        const TileDeal d = tile_deal(ntx, nty, nranks);
+        for (int ty = 0; ty < nty; ++ty)
+                for (int tx = 0; tx < ntx; ++tx) {
+                        int r, k;
+                        deal_slot(d, tx, ty, r, k);
+                        rank_of_tile[ty * ntx + tx] = r;
+                        slot_of_tile[ty * ntx + tx] = k;
+                        // the forward map must invert it
+                        int bx = -1, by = -1;
+                        if (k < deal_count(d, r))
+                                deal_tile(d, r, k, bx, by);
+                        if (bx != tx || by != ty)
+                                return fail(VRT_E_INVALID, "tile deal does not invert at (%d, %d)", tx, ty);
+                }
+        return VRT_OK;
 }
 
 static std::atomic<int> g_test_flags{0};
@@ -939,8 +972,7 @@ static void fill_render_params(vrt_scene *s, const vrt_camera *cam,
         p->nty = film->ny / 8;
         p->rank = rank;
         p->nranks = nranks;
-        const int T = p->ntx * p->nty;
-        p->tiles_this_rank = rank < T ? (T - rank + nranks - 1) / nranks : 0;
+        p->tiles_this_rank = deal_count(tile_deal(p->ntx, p->nty, nranks), rank);
         p->test_flags = g_test_flags.load();
 }
 

@@ -128,6 +128,92 @@ __host__ __device__ inline void queue_range(int units, int x, int &lo, int &hi)
                 hi = lo;
 }
 
+// Tile deal of a multi-rank frame.  The ntx x nty grid of
+// 8x8-pixel tiles is cut into G x G blocks of tiles (G = VRT_DEAL_BLOCK);
+// the whole blocks are dealt round-robin in block raster order (block j ->
+// rank j % nranks), then the tiles outside the whole-block region -- the
+// right strip (rows above the bottom strip), then the bottom strip, each in
+// raster order -- continue the round robin one tile at a time (leftover i ->
+// rank (F + i) % nranks, F = whole blocks).  A rank's tiles are numbered k =
+// 0, 1, ...: its blocks' tiles (block order, row-major inside a block), then
+// its leftover tiles.  A rank's share is so made of compact G x G regions
+// (rays of one region walk the same part of the octree), and every rank gets
+// the same number of blocks +-1.  G = 1 is tile t -> rank t % nranks.
+#ifndef VRT_DEAL_BLOCK
+#define VRT_DEAL_BLOCK 4
+#endif
+struct TileDeal {
+        int ntx, nty, nranks, G;
+        int bx, by;  // whole blocks per block row / per block column
+        int F;       // whole blocks
+        int rw;      // width of the right strip (ntx - bx*G)
+        int nA;      // tiles of the right strip
+        int L;       // leftover tiles (right strip + bottom strip)
+};
+__host__ __device__ inline TileDeal tile_deal(int ntx, int nty, int nranks)
+{
+        TileDeal d;
+        d.ntx = ntx;
+        d.nty = nty;
+        d.nranks = nranks;
+        d.G = nranks > 1 ? VRT_DEAL_BLOCK : 1;  // one rank: raster order
+        d.bx = ntx / d.G;
+        d.by = nty / d.G;
+        d.F = d.bx * d.by;
+        d.rw = ntx - d.bx * d.G;
+        d.nA = d.by * d.G * d.rw;
+        d.L = ntx * nty - d.F * d.G * d.G;
+        return d;
+}
+// whole blocks of rank r, and the first leftover index it owns
+__host__ __device__ inline int deal_blocks(const TileDeal &d, int r)
+{
+        return r < d.F ? (d.F - r + d.nranks - 1) / d.nranks : 0;
+}
+__host__ __device__ inline int deal_l0(const TileDeal &d, int r)
+{
+        return ((r - d.F) % d.nranks + d.nranks) % d.nranks;
+}
+// tiles of rank r
+__host__ __device__ inline int deal_count(const TileDeal &d, int r)
+{
+        const int l0 = deal_l0(d, r);
+        return deal_blocks(d, r) * d.G * d.G + (l0 < d.L ? (d.L - l0 + d.nranks - 1) / d.nranks : 0);
+}
+// rank r's k-th tile -> (tx, ty)
+__host__ __device__ inline void deal_tile(const TileDeal &d, int r, int k, int &tx, int &ty)
+{
+        const int G2 = d.G * d.G, nb = deal_blocks(d, r);
+        if (k < nb * G2) {
+                const int j = r + (k / G2) * d.nranks, w = k % G2;
+                tx = (j % d.bx) * d.G + w % d.G;
+                ty = (j / d.bx) * d.G + w / d.G;
+                return;
+        }
+        int li = deal_l0(d, r) + (k - nb * G2) * d.nranks;
+        if (li < d.nA) {
+                ty = li / d.rw;
+                tx = d.bx * d.G + li % d.rw;
+        } else {
+                li -= d.nA;
+                ty = d.by * d.G + li / d.ntx;
+                tx = li % d.ntx;
+        }
+}
+// tile (tx, ty) -> its rank r and index k there
+__host__ __device__ inline void deal_slot(const TileDeal &d, int tx, int ty, int &r, int &k)
+{
+        if (tx < d.bx * d.G && ty < d.by * d.G) {
+                const int j = (ty / d.G) * d.bx + tx / d.G;
+                r = j % d.nranks;
+                k = (j / d.nranks) * d.G * d.G + (ty % d.G) * d.G + tx % d.G;
+                return;
+        }
+        const int li = ty < d.by * d.G ? ty * d.rw + (tx - d.bx * d.G) : d.nA + (ty - d.by * d.G) * d.ntx + tx;
+        r = (d.F + li) % d.nranks;
+        k = deal_blocks(d, r) * d.G * d.G + li / d.nranks;
+}
+
 // Unit order of a persistent launch: 2^sh units per 8x8-pixel tile (the 4
 // quadrants of a primary render, the 64 pixels of a config-5 launch).  When
 // this rank's tiles form an exact grid (vw columns x rows: one rank, or a
@@ -151,7 +237,7 @@ __host__ __device__ inline UnitMap unit_map(int ntx, int nty, int nranks, int ti
         m.vw = ntx / nranks;
         m.rows = nty;
         m.sh = sh;
-        m.strips = VRT_STRIPS && ntx % nranks == 0 && m.vw * nty == tiles && m.vw >= 8;
+        m.strips = VRT_STRIPS && nranks == 1 && m.vw * nty == tiles && m.vw >= 8;
         return m;
 }
 __host__ __device__ inline void slice_range(const UnitMap &m, int x, int &lo, int &hi)
@@ -196,7 +282,7 @@ struct RenderParams {
         DevScene sc;
         CamParams cam;
         int32_t ntx, nty;      // 8x8 tiles in the render area
-        int32_t rank, nranks;  // tile t handled by rank t % nranks
+        int32_t rank, nranks;  // this rank's tiles: tile_deal / deal_tile
         int32_t tiles_this_rank;
         int32_t image_layout;  // 1: out is nx*ny*3 image; 0: packed tiles
         int32_t test_flags;    // vrt_set_test_flags (VRT_TEST_FORCE_DEFER)

@@ -1249,8 +1249,8 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                 return l;
         };
         const CamParams &c = p.cam;
-        const int t = p.rank + k * p.nranks;
-        const int tx = t % p.ntx, ty = t / p.ntx;
+        int tx, ty;
+        deal_tile(tile_deal(p.ntx, p.nty, p.nranks), p.rank, k, tx, ty);
         // pixel, sample and Camera::gen_rays4 direction (VRT/camera.cc:95-112)
         // of lane l
         auto sample_of = [&](int l, int &px, int &py, int &s, int &lx, int &ly) {
@@ -1617,7 +1617,7 @@ __global__ __launch_bounds__(kBlock) void k_primary1(RenderParams p, float *__re
 struct SecondaryParams {
         DevScene sc;
         int32_t nx, W8, H8, spp;
-        int32_t rank, nranks;  // 8x8 tile t handled when t % nranks == rank
+        int32_t rank, nranks;  // this rank's 8x8 tiles: tile_deal
         float res;
         const float *prim;
         float *vis;            // nx*ny, this rank's pixels written
@@ -1646,14 +1646,14 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
 {
         // lane id re-read per pixel (not held across k_secondary_p's loop)
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-        // this rank's tile kt = k / 64 (8x8-pixel tiles dealt round-robin:
-        // tile t -> rank t % nranks, as the primary render), pixel k % 64
-        // of it, row-major
-        const int ntx = p.W8 >> 3;
-        const int64_t t = (k >> 6) * p.nranks + p.rank;
-        if (t >= (int64_t)ntx * (p.H8 >> 3))
+        // this rank's tile k / 64 (the 8x8-pixel tiles dealt as the primary
+        // render's, tile_deal), pixel k % 64 of it, row-major
+        const TileDeal dl = tile_deal(p.W8 >> 3, p.H8 >> 3, p.nranks);
+        if ((k >> 6) >= (int64_t)deal_count(dl, p.rank))
                 return;
-        const int px = (int)(t % ntx) * 8 + (int)(k & 7), py = (int)(t / ntx) * 8 + (int)((k >> 3) & 7);
+        int tx, ty;
+        deal_tile(dl, p.rank, (int)(k >> 6), tx, ty);
+        const int px = tx * 8 + (int)(k & 7), py = ty * 8 + (int)((k >> 3) & 7);
         const int64_t pix = (int64_t)py * p.W8 + px;
         const float *pr = p.prim + 8 * pix;
         const size_t vi = (size_t)py * p.nx + px;
@@ -1783,9 +1783,8 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
         sp.s_hit = s_hit;
         sp.s_tri = s_tri;
         sp.s_vox = s_vox;
-        // pixels of this rank: its 8x8 tiles (tile t -> rank t % nranks)
-        const int64_t ntiles = npix / 64;
-        const int64_t mine = rank < ntiles ? (ntiles - rank + nranks - 1) / nranks : 0;
+        // pixels of this rank: its 8x8 tiles (tile_deal)
+        const int64_t mine = deal_count(tile_deal(rp.ntx, rp.nty, nranks), rank);
         const int64_t waves = mine * 64;
         if (waves == 0)
                 return hipGetLastError();
@@ -1830,8 +1829,8 @@ __global__ void k_unpack(int nx, int ny, int ntx, int nty, int nranks,
         const int tx = px >> 3, ty = py >> 3;
         float v0 = 0.f, v1 = 0.f, v2 = 0.f;
         if (tx < ntx && ty < nty) {
-                const int t = ty * ntx + tx;
-                const int r = t % nranks, k = t / nranks;
+                int r, k;
+                deal_slot(tile_deal(ntx, nty, nranks), tx, ty, r, k);
                 const float *q = src + (((int64_t)r * tpr + k) * 64 + (py & 7) * 8 + (px & 7)) * 3;
                 v0 = q[0];
                 v1 = q[1];
@@ -2147,8 +2146,8 @@ __device__ __forceinline__ bool tile_lane(const RenderParams &p, int &k, int &px
         if (u >= p.tiles_this_rank * kQ)
                 return false;
         k = u / kQ;
-        const int t = p.rank + k * p.nranks;
-        const int tx = t % p.ntx, ty = t / p.ntx;
+        int tx, ty;
+        deal_tile(tile_deal(p.ntx, p.nty, p.nranks), p.rank, k, tx, ty);
         const int tid = threadIdx.x, wave = (u % kQ) * VRT_RENDER_WAVES + (tid >> 6), lane = tid & 63;
         s = lane & 3;
         const int pix = lane >> 2;
@@ -2627,8 +2626,8 @@ __global__ __launch_bounds__(256) void k_trace_film(TraceParams p, int64_t npix_
         const int u = (int)(slot0 / kRenderBlock);
         const int tid0 = (int)(slot0 % kRenderBlock);
         const int k = u / kQ;
-        const int t = p.r.rank + k * p.r.nranks;
-        const int tx = t % p.r.ntx, ty = t / p.r.ntx;
+        int tx, ty;
+        deal_tile(tile_deal(p.r.ntx, p.r.nty, p.r.nranks), p.r.rank, k, tx, ty);
         const int wave = (u % kQ) * VRT_RENDER_WAVES + (tid0 >> 6);
         const int pix = (tid0 & 63) >> 2;
         const int lx = (wave & 1) * 4 + (pix & 3), ly = (wave >> 1) * 4 + (pix >> 2);

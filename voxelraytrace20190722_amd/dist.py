@@ -7,13 +7,20 @@ layouts on the host.  They are the reference for tests/test_dist.py (gloo,
 world_size 2, CPU) and the host-staged gloo rehearsal of bench.py, and
 tests/test_gpu.py checks that the device buffers equal them bit for bit.
 
-Primary frames: the render area is 8x8-pixel tiles t = ty*ntx + tx (ntx =
-nx//8, nty = ny//8); tile t belongs to rank t % nranks; a rank's buffer holds
-its tiles in order k = 0.. (t = rank + k*nranks), 64 pixels each, row-major
-inside the tile, 3 floats per pixel, `tiles_per_rank * 192` floats (unused
-tail zero).  Secondary frames (config 5): the same tile deal (tile t ->
-rank t % nranks); every rank writes only the pixels of its tiles into a
-zeroed image, so a SUM reduce re-assembles it exactly.
+The tile deal (include/vrt.h, vrt_internal.h `tile_deal`): the render area
+is the ntx x nty grid of 8x8-pixel tiles (ntx = nx//8, nty = ny//8).  With
+G = the library's deal block (G = 1 for one rank), the whole G x G blocks of
+tiles are dealt round-robin in block raster order (block j -> rank
+j % nranks); the tiles outside the whole-block region -- the right strip
+(rows above the bottom strip), then the bottom strip, each in raster order
+-- continue the deal one tile at a time (leftover i -> rank (F + i) %
+nranks, F = whole blocks).  A rank's k-th tile: its blocks' tiles first
+(block order, row-major inside a block), then its leftover tiles.  A rank's
+buffer holds its tiles in that order, 64 pixels each, row-major inside the
+tile, 3 floats per pixel, `tiles_per_rank * 192` floats (the largest share;
+unused tail zero).  Secondary frames (config 5): the same deal; every rank
+writes only the pixels of its tiles into a zeroed image, so a SUM reduce
+re-assembles it exactly.
 """
 import numpy as np
 
@@ -22,48 +29,84 @@ def tile_grid(nx, ny):
     return nx // 8, ny // 8
 
 
-def tiles_per_rank(nx, ny, nranks):
-    """== vrt_tiles_per_rank (ceil(ntiles / nranks))."""
+def deal_block():
+    """G of the library's tile deal (vrt_tile_deal_block)."""
+    from ._ffi import lib
+    return int(lib().vrt_tile_deal_block())
+
+
+def deal_owner(nx, ny, nranks, g=None):
+    """(nty, ntx) arrays: each tile's rank and its index k in that rank's list."""
     ntx, nty = tile_grid(nx, ny)
-    return (ntx * nty + nranks - 1) // nranks
+    g = (deal_block() if g is None else g) if nranks > 1 else 1
+    bx, by = ntx // g, nty // g
+    nfull = bx * by
+    rank = np.zeros((nty, ntx), np.int64)
+    slot = np.zeros((nty, ntx), np.int64)
+    counts = np.zeros(nranks, np.int64)
+    for j in range(nfull):  # whole blocks, block raster order
+        r = j % nranks
+        y0, x0 = (j // bx) * g, (j % bx) * g
+        for w in range(g * g):
+            ty, tx = y0 + w // g, x0 + w % g
+            rank[ty, tx] = r
+            slot[ty, tx] = counts[r]
+            counts[r] += 1
+    leftovers = [(ty, tx) for ty in range(by * g) for tx in range(bx * g, ntx)]
+    leftovers += [(ty, tx) for ty in range(by * g, nty) for tx in range(ntx)]
+    for i, (ty, tx) in enumerate(leftovers):
+        r = (nfull + i) % nranks
+        rank[ty, tx] = r
+        slot[ty, tx] = counts[r]
+        counts[r] += 1
+    return rank, slot, counts
 
 
-def rank_tiles(nx, ny, rank, nranks):
-    ntx, nty = tile_grid(nx, ny)
-    return np.arange(rank, ntx * nty, nranks)
+def tiles_per_rank(nx, ny, nranks, g=None):
+    """== vrt_tiles_per_rank (the largest share)."""
+    return int(deal_owner(nx, ny, nranks, g)[2].max()) if (nx // 8) * (ny // 8) else 0
 
 
-def pack_tiles_host(img, rank, nranks):
+def rank_tiles(nx, ny, rank, nranks, g=None):
+    """This rank's tiles (ty*ntx + tx) in its order k = 0, 1, ..."""
+    ntx, _ = tile_grid(nx, ny)
+    rk, sl, cnt = deal_owner(nx, ny, nranks, g)
+    ty, tx = np.nonzero(rk == rank)
+    order = np.argsort(sl[ty, tx])
+    return (ty * ntx + tx)[order]
+
+
+def pack_tiles_host(img, rank, nranks, g=None):
     """This rank's packed tile buffer from a full (ny, nx, 3) image."""
     ny, nx = img.shape[:2]
     ntx, _ = tile_grid(nx, ny)
-    tpr = tiles_per_rank(nx, ny, nranks)
+    tpr = tiles_per_rank(nx, ny, nranks, g)
     buf = np.zeros((tpr, 64, 3), np.float32)
-    for k, t in enumerate(rank_tiles(nx, ny, rank, nranks)):
+    for k, t in enumerate(rank_tiles(nx, ny, rank, nranks, g)):
         tx, ty = t % ntx, t // ntx
         buf[k] = img[ty * 8:ty * 8 + 8, tx * 8:tx * 8 + 8].reshape(64, 3)
     return buf.reshape(-1)
 
 
-def unpack_tiles_host(gathered, nx, ny, nranks):
+def unpack_tiles_host(gathered, nx, ny, nranks, g=None):
     """== vrt_unpack_tiles_device: (nranks, tiles_per_rank*192) -> (ny, nx, 3);
     pixels outside the tile grid are zero."""
     ntx, nty = tile_grid(nx, ny)
-    tpr = tiles_per_rank(nx, ny, nranks)
-    g = np.asarray(gathered, np.float32).reshape(nranks, tpr, 8, 8, 3)
+    tpr = tiles_per_rank(nx, ny, nranks, g)
+    rk, sl, _ = deal_owner(nx, ny, nranks, g)
+    gg = np.asarray(gathered, np.float32).reshape(nranks, tpr, 8, 8, 3)
     img = np.zeros((ny, nx, 3), np.float32)
-    for t in range(ntx * nty):
-        r, k = t % nranks, t // nranks
-        tx, ty = t % ntx, t // ntx
-        img[ty * 8:ty * 8 + 8, tx * 8:tx * 8 + 8] = g[r, k]
+    for ty in range(nty):
+        for tx in range(ntx):
+            img[ty * 8:ty * 8 + 8, tx * 8:tx * 8 + 8] = gg[rk[ty, tx], sl[ty, tx]]
     return img
 
 
-def secondary_mask(nx, ny, rank, nranks):
+def secondary_mask(nx, ny, rank, nranks, g=None):
     """(ny, nx) bool: the pixels `rank` computes in a config-5 frame."""
     ntx, nty = tile_grid(nx, ny)
-    t = np.arange(ntx * nty).reshape(nty, ntx)
-    mine = np.repeat(np.repeat((t % nranks) == rank, 8, 0), 8, 1)
+    rk, _, _ = deal_owner(nx, ny, nranks, g)
+    mine = np.repeat(np.repeat(rk == rank, 8, 0), 8, 1)
     m = np.zeros((ny, nx), bool)
     m[:nty * 8, :ntx * 8] = mine
     return m
