@@ -119,7 +119,7 @@ def run_pmc(a, kernel_prefix, save_dir=""):
         out_dir = os.path.join(tmp, name)
         cmd = [prof, "--pmc", *counters, "--output-format", "csv", "-d", out_dir, "-o", name, "--",
                sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-counters", "--no-pmc",
-               "--no-d9", "--warmup", "0", "--steps", str(a.steps), *workload_args(a)]
+               "--no-d9", "--frames-in-flight", "1", "--warmup", "0", "--steps", str(a.steps), *workload_args(a)]
         t0 = time.time()
         p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                              start_new_session=True, text=True)
@@ -155,7 +155,7 @@ def run_pmc(a, kernel_prefix, save_dir=""):
 def roofline_from_pmc(pmc, kernel_ms, out_bytes, ref_bytes):
     """The measured roofline of the dominant kernel: VALU issue (the limiter,
     DESIGN.md §4) -- the VALU wave-instructions of one launch (SQ_INSTS_VALU)
-    over this run's HIP-event kernel time, against the issue peak at the max
+    over this run's per-frame device time (frame_ms), against the issue peak at the max
     engine clock -- and HBM traffic (FETCH_SIZE x2 per MI355X_MICROARCH.md
     §HBM + WRITE_SIZE; rocprofv3 reports KiB) over the same time as a
     fraction of the 8 TB/s peak.  issue_frac_at_clock is the same
@@ -260,6 +260,9 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (RCCL over xGMI, the real path) or gloo (host-staged rehearsal)")
     p.add_argument("--save-image", default="", help="rank 0 writes the last frame as .hdr")
+    p.add_argument("--frames-in-flight", type=int, default=2,
+                   help="consecutive frames on this many HIP streams (own output buffers), so a frame's "
+                        "ramp-down overlaps the next frame's launch; 1 = one stream")
     p.add_argument("--rehearse-ranks", type=int, default=0,
                    help="single-GPU rehearsal of the N-rank path (WORLD_SIZE 1): render rank 0's share of the "
                         "tiles as one of R ranks, RCCL gather over a 1-rank process group, unpack of R rank "
@@ -338,79 +341,101 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
+    # frames in flight: frame k runs on streams[k % nfl] with its own output
+    # buffers, so frame k+1's persistent grid fills the CUs while frame k's
+    # last (latency-bound) units finish -- a launch's ramp-down is ~0.2 ms
+    # whatever its size.  Every frame is still one full launch.
+    nfl = 1 if (trace or a.dist_backend == "gloo") else max(1, a.frames_in_flight)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nfl - 1)]
     tpr = vrt.tiles_per_rank(film, nshare)
     secondary = a.mode == "secondary"
-    img = torch.zeros((a.height, a.width) if secondary else (a.height, a.width, 3), dtype=torch.float32,
-                      device=dev)
+    img_shape = (a.height, a.width) if secondary else (a.height, a.width, 3)
+    imgs = [torch.zeros(img_shape, dtype=torch.float32, device=dev) for _ in range(nfl)]
+    img = imgs[0]
+    nbuf = max(2, nfl)  # multi-rank buffers: one per frame in flight (>= 2: gather k overlaps frame k+1)
     if secondary:
         # config 5: rays per frame are data dependent (64 per primary hit):
         # count them per pose once, outside the timed region
         frame_rays = {}
         for pi in sorted({k % a.poses for k in range(a.steps)}):
             _, frame_rays[pi] = tree.render_secondary(cams[pi], film, spp=a.spp)
-        prim = torch.zeros(W8 * H8 * 8, dtype=torch.float32, device=dev)
-        visb = [torch.zeros((a.height, a.width), dtype=torch.float32, device=dev) for _ in range(2)]
+        prims = [torch.zeros(W8 * H8 * 8, dtype=torch.float32, device=dev) for _ in range(nbuf)]
+        visb = [torch.zeros((a.height, a.width), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     elif nshare > 1:
-        # double-buffered: the RCCL gather of frame k (on the NCCL stream)
-        # overlaps the render of frame k+1 (on the compute stream)
-        tiles = [torch.zeros(tpr * 192, dtype=torch.float32, device=dev) for _ in range(2)]
-        gathered = ([torch.zeros((nshare, tpr * 192), dtype=torch.float32, device=dev) for _ in range(2)]
+        # the RCCL gather of frame k (on the NCCL stream) overlaps the render
+        # of frame k+1
+        tiles = [torch.zeros(tpr * 192, dtype=torch.float32, device=dev) for _ in range(nbuf)]
+        gathered = ([torch.zeros((nshare, tpr * 192), dtype=torch.float32, device=dev) for _ in range(nbuf)]
                     if rank == 0 else None)
         # in-place views (a rehearsal's 1-rank group gathers into row 0 only)
-        gl = [list(g[:world].unbind(0)) for g in gathered] if rank == 0 else [None, None]
-    works = [None, None]
+        gl = [list(g[:world].unbind(0)) for g in gathered] if rank == 0 else [None] * nbuf
+    works = [None] * nbuf
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(a.steps)]
 
-    def finish(b):
-        """Rank 0: re-assemble the frame gathered into buffer b."""
+    def sl(k):
+        """frame k's stream slot and buffer slot"""
+        return k % nfl, k % nbuf
+
+    def finish(b, s):
+        """Rank 0: re-assemble the frame gathered into buffer b, on stream s."""
         if works[b] is None:
             return
-        works[b].wait()  # stream-wait on the collective, no host block
+        with torch.cuda.stream(s):
+            works[b].wait()  # stream-wait on the collective, no host block
         works[b] = None
         if rank == 0:
             if secondary:
-                img.copy_(visb[b])
+                with torch.cuda.stream(s):
+                    imgs[0].copy_(visb[b])
             else:
-                vrt.unpack_tiles_device(film, nshare, gathered[b].data_ptr(), img.data_ptr(), sp)
+                vrt.unpack_tiles_device(film, nshare, gathered[b].data_ptr(), imgs[0].data_ptr(), s.cuda_stream)
 
     def step_secondary(k, timed):
         cam = cams[k % a.poses]
+        j, b = sl(k)
+        s = streams[j]
         if timed:
-            ev[k][0].record(stream)
+            ev[k][0].record(s)
         if world == 1:
-            tree.render_secondary_device(cam, film, a.spp, 0, 1, prim.data_ptr(), img.data_ptr(), sp)
+            tree.render_secondary_device(cam, film, a.spp, 0, 1, prims[j].data_ptr(), imgs[j].data_ptr(),
+                                         s.cuda_stream)
             if timed:
-                ev[k][1].record(stream)
+                ev[k][1].record(s)
             return
-        b = k & 1
-        finish(b)
+        finish(b, s)  # frame k - nbuf used these buffers (normally finished already)
         if rank == 0:
-            visb[b].zero_()  # the previous reduce summed into rank 0's buffer
-        # each rank writes only its own pixels (8x8 tiles dealt round-robin);
-        # the others stay +0.0, so a SUM reduce assembles the image exactly
-        tree.render_secondary_device(cam, film, a.spp, rank, world, prim.data_ptr(), visb[b].data_ptr(), sp)
+            with torch.cuda.stream(s):
+                visb[b].zero_()  # the previous reduce summed into rank 0's buffer
+        # each rank writes only its own pixels (its tiles of the deal); the
+        # others stay +0.0, so a SUM reduce assembles the image exactly
+        tree.render_secondary_device(cam, film, a.spp, rank, world, prims[b].data_ptr(), visb[b].data_ptr(),
+                                     s.cuda_stream)
         if timed:
-            ev[k][1].record(stream)
+            ev[k][1].record(s)
         if a.dist_backend == "nccl":
-            works[b] = dist.reduce(visb[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
-            finish(1 - b)
+            with torch.cuda.stream(s):
+                works[b] = dist.reduce(visb[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
+            jp, bp = sl(k - 1)
+            finish(bp, streams[jp])  # frame k-1: its reduce overlapped this render
         else:
             host = visb[b].cpu()
             dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
             if rank == 0:
                 img.copy_(host)
 
-    def render(cam, rk, nr, layout, ptr_):
+    def render(cam, rk, nr, layout, ptr_, s):
         if trace:
-            tree.render_trace_device(cam, film, rk, nr, layout, ptr_, res, sp)
+            tree.render_trace_device(cam, film, rk, nr, layout, ptr_, res, s.cuda_stream)
         else:
-            tree.render_tiles_device(cam, film, rk, nr, layout, ptr_, sp)
+            tree.render_tiles_device(cam, film, rk, nr, layout, ptr_, s.cuda_stream)
 
     def step(k, timed):
         if secondary:
             return step_secondary(k, timed)
         cam = cams[k % a.poses]
+        j, b = sl(k)
+        s = streams[j]
         if trace:
             # light pass + filter (blocking, on the scene's own stream; every
             # rank builds the whole light map -- the final render is sharded)
@@ -420,23 +445,24 @@ def main():
             if timed:
                 light_ms.append((time.perf_counter() - t0_) * 1e3)
         if timed:
-            ev[k][0].record(stream)
+            ev[k][0].record(s)
         if nshare == 1:
-            render(cam, 0, 1, 1, img.data_ptr())
+            render(cam, 0, 1, 1, imgs[j].data_ptr(), s)
             if timed:
-                ev[k][1].record(stream)
+                ev[k][1].record(s)
             return
-        b = k & 1
-        finish(b)  # frame k-2 used this buffer pair (normally finished already)
-        render(cam, rank, nshare, 0, tiles[b].data_ptr())
+        finish(b, s)  # frame k - nbuf used this buffer pair (normally finished already)
+        render(cam, rank, nshare, 0, tiles[b].data_ptr(), s)
         if timed:
-            ev[k][1].record(stream)
+            ev[k][1].record(s)
         if a.dist_backend == "nccl":
             # frame k's gather is queued as soon as its render is: the NCCL
             # stream waits for this render only, so its kernel is ready before
-            # render k+1 (queued after frame k-1's unpack) and runs beside it
-            works[b] = dist.gather(tiles[b], gl[b], dst=0, async_op=True)
-            finish(1 - b)  # frame k-1: its gather overlapped this render
+            # the next frame's render and runs beside it
+            with torch.cuda.stream(s):
+                works[b] = dist.gather(tiles[b], gl[b], dst=0, async_op=True)
+            jp, bp = sl(k - 1)
+            finish(bp, streams[jp])  # frame k-1: its gather overlapped this render
         else:  # gloo rehearsal (several ranks on one GPU): host-staged gather
             host = tiles[b].cpu()
             hl = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
@@ -446,8 +472,8 @@ def main():
                 vrt.unpack_tiles_device(film, world, gathered[b].data_ptr(), img.data_ptr(), sp)
 
     def drain():
-        finish(0)
-        finish(1)
+        for b in range(nbuf):
+            finish(b, stream)
 
     for k in range(a.warmup):
         step(k, False)
@@ -469,7 +495,11 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kms = np.array([s.elapsed_time(e) for s, e in ev])  # render kernel, ms
+    kms = np.array([s.elapsed_time(e) for s, e in ev])  # render launch span (HIP events on its stream), ms
+    # per-frame device time: the launch span with one frame in flight; with
+    # several, spans overlap (a span also holds the wait for the CUs the
+    # previous frame still occupies), so the frame time is the step time
+    frame_ms = float(kms.mean()) if nfl == 1 else elapsed * 1e3 / a.steps
 
     # ---- algorithmic bytes from the instrumented kernel's
     # reference-equivalent counters, per pose actually rendered
@@ -479,17 +509,19 @@ def main():
     d9 = None
     if world == 1 and not rehearse and not secondary and not trace and not a.no_d9:
         tree9 = vrt.VoxelOctree(sd, a.depth + 1, device=local)
-        img9 = torch.zeros_like(img)
+        img9 = [torch.zeros_like(img) for _ in range(nfl)]
         for k in range(a.warmup):
-            tree9.render_tiles_device(cams[k % a.poses], film, 0, 1, 1, img9.data_ptr(), sp)
+            tree9.render_tiles_device(cams[k % a.poses], film, 0, 1, 1, img9[k % nfl].data_ptr(),
+                                      streams[k % nfl].cuda_stream)
         ev9 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(a.steps)]
         torch.cuda.synchronize()
         t9 = time.perf_counter()
-        for k in range(a.steps):
-            ev9[k][0].record(stream)
-            tree9.render_tiles_device(cams[k % a.poses], film, 0, 1, 1, img9.data_ptr(), sp)
-            ev9[k][1].record(stream)
+        for k in range(a.steps):  # the same frames-in-flight schedule as the headline
+            s9 = streams[k % nfl]
+            ev9[k][0].record(s9)
+            tree9.render_tiles_device(cams[k % a.poses], film, 0, 1, 1, img9[k % nfl].data_ptr(), s9.cuda_stream)
+            ev9[k][1].record(s9)
         torch.cuda.synchronize()
         e9 = time.perf_counter() - t9
         k9 = np.mean([s.elapsed_time(e) for s, e in ev9])
@@ -551,7 +583,7 @@ def main():
         pmc, why = run_pmc(a, "k_secondary" if secondary else "k_render", a.pmc_save)
         out_bytes = (W8 * H8 * 4) if secondary else (W8 * H8 * 12 // nshare)
         if pmc:
-            roof = roofline_from_pmc(pmc, float(kms.mean()), out_bytes, ref_bytes)
+            roof = roofline_from_pmc(pmc, frame_ms, out_bytes, ref_bytes)
             if per_ray:
                 roof["per_ray"] = per_ray
             roof["build_id"] = vrt.build_id()
@@ -635,7 +667,8 @@ def main():
     data_desc = (f"OBJ scene {a.scene} (tinyobj-exact ingest)" if a.scene else
                  "synthetic: deterministic sponza-proxy atrium (sponza.obj absent)")
     if rank == 0 and a.save_image:
-        vrt.write_hdr(a.save_image, img.cpu().numpy())
+        last = imgs[(a.steps - 1) % nfl] if world == 1 and nshare == 1 else img
+        vrt.write_hdr(a.save_image, last.cpu().numpy())
     if rank == 0:
         coll = "rccl" if a.dist_backend == "nccl" else "gloo"
         n_side = int(round(2 ** a.depth))
@@ -690,7 +723,9 @@ def main():
                        "rays_per_frame": int(round(mean_rays)), "tris": sd.ntri, "poses": a.poses,
                        "parallelism": par},
             "kernel_ms_mean": round(float(kms.mean()), 4),
-            "kernel_mrays_per_s": round(mean_rays / world / (kms.mean() * 1e-3) / 1e6, 2),
+            "frames_in_flight": nfl,
+            "frame_ms": round(frame_ms, 4),
+            "kernel_mrays_per_s": round(mean_rays / world / (frame_ms * 1e-3) / 1e6, 2),
             "roofline": roof,
             "cpu_baseline": cpu,
         }
@@ -711,7 +746,7 @@ def main():
                 "note": "per-rank step time of the N-rank path (render of 1/N of the tiles, RCCL gather, unpack "
                         "of N rank buffers, Python host loop) on one GPU; a real N-GPU step adds the xGMI "
                         "transfer into rank 0"}
-            out["kernel_mrays_per_s"] = round(mean_rays / nshare / (kms.mean() * 1e-3) / 1e6, 2)
+            out["kernel_mrays_per_s"] = round(mean_rays / nshare / (frame_ms * 1e-3) / 1e6, 2)
         out["build_id"] = vrt.build_id()
         print(json.dumps(out), flush=True)
     if world > 1 or rehearse:
