@@ -263,6 +263,8 @@ def parse():
     p.add_argument("--frames-in-flight", type=int, default=2,
                    help="consecutive frames on this many HIP streams (own output buffers), so a frame's "
                         "ramp-down overlaps the next frame's launch; 1 = one stream")
+    p.add_argument("--frames-in-flight-secondary", type=int, default=1,
+                   help="frames in flight for --mode secondary (36 ms frames: 2 in flight measured 5%% slower)")
     p.add_argument("--rehearse-ranks", type=int, default=0,
                    help="single-GPU rehearsal of the N-rank path (WORLD_SIZE 1): render rank 0's share of the "
                         "tiles as one of R ranks, RCCL gather over a 1-rank process group, unpack of R rank "
@@ -346,6 +348,8 @@ def main():
     # last (latency-bound) units finish -- a launch's ramp-down is ~0.2 ms
     # whatever its size.  Every frame is still one full launch.
     nfl = 1 if (trace or a.dist_backend == "gloo") else max(1, a.frames_in_flight)
+    if a.mode == "secondary" and a.frames_in_flight_secondary is not None:
+        nfl = max(1, a.frames_in_flight_secondary)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nfl - 1)]
     tpr = vrt.tiles_per_rank(film, nshare)
     secondary = a.mode == "secondary"
@@ -384,12 +388,13 @@ def main():
         with torch.cuda.stream(s):
             works[b].wait()  # stream-wait on the collective, no host block
         works[b] = None
-        if rank == 0:
+        if rank == 0:  # each buffer slot re-assembles into its own image (frames in flight)
             if secondary:
                 with torch.cuda.stream(s):
-                    imgs[0].copy_(visb[b])
+                    imgs[b % nfl].copy_(visb[b])
             else:
-                vrt.unpack_tiles_device(film, nshare, gathered[b].data_ptr(), imgs[0].data_ptr(), s.cuda_stream)
+                vrt.unpack_tiles_device(film, nshare, gathered[b].data_ptr(), imgs[b % nfl].data_ptr(),
+                                        s.cuda_stream)
 
     def step_secondary(k, timed):
         cam = cams[k % a.poses]
@@ -486,6 +491,9 @@ def main():
     for k in range(a.steps):
         step(k, True)
     drain()
+    # host time to enqueue the K steps: close to `elapsed` means the host
+    # loop, not the GPU, sets the pace
+    host_enq = time.perf_counter() - t_start
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -667,7 +675,7 @@ def main():
     data_desc = (f"OBJ scene {a.scene} (tinyobj-exact ingest)" if a.scene else
                  "synthetic: deterministic sponza-proxy atrium (sponza.obj absent)")
     if rank == 0 and a.save_image:
-        last = imgs[(a.steps - 1) % nfl] if world == 1 and nshare == 1 else img
+        last = imgs[(a.steps - 1) % nfl] if nfl > 1 else img
         vrt.write_hdr(a.save_image, last.cpu().numpy())
     if rank == 0:
         coll = "rccl" if a.dist_backend == "nccl" else "gloo"
@@ -724,6 +732,7 @@ def main():
                        "parallelism": par},
             "kernel_ms_mean": round(float(kms.mean()), 4),
             "frames_in_flight": nfl,
+            "host_enqueue_ms_per_step": round(host_enq * 1e3 / a.steps, 4),
             "frame_ms": round(frame_ms, 4),
             "kernel_mrays_per_s": round(mean_rays / world / (frame_ms * 1e-3) / 1e6, 2),
             "roofline": roof,
