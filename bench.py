@@ -260,7 +260,7 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (RCCL over xGMI, the real path) or gloo (host-staged rehearsal)")
     p.add_argument("--save-image", default="", help="rank 0 writes the last frame as .hdr")
-    p.add_argument("--frames-in-flight", type=int, default=2,
+    p.add_argument("--frames-in-flight", type=int, default=3,
                    help="consecutive frames on this many HIP streams (own output buffers), so a frame's "
                         "ramp-down overlaps the next frame's launch; 1 = one stream")
     p.add_argument("--frames-in-flight-secondary", type=int, default=1,

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 
@@ -1164,35 +1165,9 @@ __device__ __forceinline__ bool ray_occluded_dispatch(const DevScene &sc, const 
         return ray_occluded<false, kS, kR64>(sc, r, stk);
 }
 
-// Material and texture tables staged in LDS by the persistent primary
-// render (lds_tables) when the scene has at most kLdsMats / kLdsTexs of
-// them: the shading chain triangle attributes -> material -> texture record
-// -> texel then makes two dependent global loads instead of four.
-#ifndef VRT_LDS_TABLES
-#define VRT_LDS_TABLES 1
-#endif
-constexpr int kLdsMats = 64, kLdsTexs = 64;
-__shared__ MatRec g_lds_mats[kLdsMats];
-__shared__ TexRec g_lds_texs[kLdsTexs];
-__device__ __forceinline__ bool lds_tables(const DevScene &sc)
-{
-        const bool ok = VRT_LDS_TABLES && sc.nmat <= kLdsMats && sc.ntex <= kLdsTexs;
-        if (ok) {
-                for (int i = threadIdx.x; i < sc.nmat; i += blockDim.x)
-                        g_lds_mats[i] = sc.mats[i];
-                for (int i = threadIdx.x; i < sc.ntex; i += blockDim.x)
-                        g_lds_texs[i] = sc.texs[i];
-        }
-        __syncthreads();
-        return ok;
-}
-
 // Triangle::get_albedo (VRT/voxel_octree.cc:472-484) with Triangle::isect's
-// normal (VRT/voxel_octree.cc:451-453).  kTabs: the material / texture
-// records come from the LDS tables when `tabs` (lds_tables) says they hold
-// them.
-template <bool kTabs = false>
-__device__ __forceinline__ f3 hit_albedo(const DevScene &sc, const MarchResult &m, f3 &normal, bool tabs = false)
+// normal (VRT/voxel_octree.cc:451-453).
+__device__ __forceinline__ f3 hit_albedo(const DevScene &sc, const MarchResult &m, f3 &normal)
 {
         const TriAttr *ta = sc.tri_attr + m.tri;
         const float4 *q = reinterpret_cast<const float4 *>(ta);
@@ -1204,7 +1179,7 @@ __device__ __forceinline__ f3 hit_albedo(const DevScene &sc, const MarchResult &
         const int mat = __float_as_int(a3.w);
         const float w = clampf(1.0f - m.u - m.v, 0, 1);
         normal = normalize((n0 * w + n1 * m.u) + n2 * m.v);
-        const MatRec mr = (kTabs && tabs) ? g_lds_mats[mat] : sc.mats[mat];
+        const MatRec mr = sc.mats[mat];
         f3 albedo;
         if (mr.tex < 0) {
                 albedo = mk3(mr.kd[0], mr.kd[1], mr.kd[2]);
@@ -1219,7 +1194,7 @@ __device__ __forceinline__ f3 hit_albedo(const DevScene &sc, const MarchResult &
                 bc.z = clampf(bc.z, 0.f, 1.f);
                 const float tu = (bc.x * t0u + bc.y * t1u) + bc.z * t2u;
                 const float tv = (bc.x * t0v + bc.y * t1v) + bc.z * t2v;
-                const TexRec tx = (kTabs && tabs) ? g_lds_texs[mr.tex] : sc.texs[mr.tex];
+                const TexRec tx = sc.texs[mr.tex];
                 const int x = clampi((int)(unit_cycle(tu) * (float)tx.w), 0, tx.w - 1);
                 int y = clampi((int)(unit_cycle(tv) * (float)tx.h), 0, tx.h - 1);
                 y = tx.h - 1 - y;
@@ -1234,11 +1209,10 @@ __device__ __forceinline__ f3 hit_albedo(const DevScene &sc, const MarchResult &
 }
 
 // Triangle::get_diffuse(isect, ray, (1,1,1)) (VRT/voxel_octree.cc:462-470)
-template <bool kTabs = false>
 __device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
-                                        const MarchResult &m, f3 &normal, bool tabs = false)
+                                        const MarchResult &m, f3 &normal)
 {
-        const f3 albedo = hit_albedo<kTabs>(sc, m, normal, tabs);
+        const f3 albedo = hit_albedo(sc, m, normal);
         float tmp = dot(normal, -r.d);
         tmp = clampf(tmp, 0.f, 1.f);
         const f3 c = albedo * tmp;
@@ -1262,10 +1236,9 @@ constexpr int kRenderBlock = 64 * VRT_RENDER_WAVES;
 // standard-range instantiation is compiled in (fewer live registers); a wave
 // whose rays need another path returns false before writing anything and the
 // caller defers the unit to k_render_defer.
-template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kNS = 0,
-          bool kTabs = false>
+template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kNS = 0>
 __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wave, int lane, uint2 *stk,
-                                            uint32_t *stk_aux, uint32_t *path_rem, bool tabs = false)
+                                            uint32_t *stk_aux, uint32_t *path_rem)
 {
         // the lane id is re-read per unit (volatile asm: not hoisted out of
         // a persistent loop), so its derived per-lane constants are
@@ -1320,7 +1293,7 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                 f3 nrm;
                 RayK rs;  // shade_hit reads the direction only
                 rs.d = dn;
-                col = shade_hit<kTabs>(p.sc, rs, m, nrm, tabs);
+                col = shade_hit(p.sc, rs, m, nrm);
         } else {
                 col = sky(dn.y);
         }
@@ -1454,7 +1427,6 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
         constexpr int kNS = kFastOnly ? VRT_LDS_NODES : 0;
         __shared__ uint2 stk[kStack * kPersistBlock];
         stage_nodes<kNS>(p.sc.nodes, p.sc.nnodes);
-        const bool tabs = lds_tables(p.sc);
         const int tid = threadIdx.x, lane = tid & 63;
         const UnitMap um = unit_map(p.ntx, p.nty, p.nranks, p.tiles_this_rank, 2);
         const int xcd = blockIdx.x & 7;
@@ -1472,8 +1444,8 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
 #if VRT_PHASE_STAMPS
                         const unsigned long long d_u0 = __builtin_amdgcn_s_memtime();
 #endif
-                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kNS, true>(
-                                p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr, tabs);
+                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kNS>(
+                                p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr);
 #if VRT_PHASE_STAMPS
                         if (lane == 0)
                                 atomicAdd(&g_phase[10], __builtin_amdgcn_s_memtime() - d_u0);
@@ -2040,8 +2012,16 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 // 4 units, a multiple of 8 for the XCD map)
                 const int need = (p.tiles_this_rank + 7) & ~7;  // 4 units per tile, 4 waves per block
                 // (kCollectiveReserve: room for the RCCL gather of the previous frame)
-                const int cap = p.nranks > 1 ? std::max(8, p.sc.persist_blocks - kCollectiveReserve)
-                                             : p.sc.persist_blocks;
+                // VRT_PERSIST_GRID_DIV (tuning knob, read once): a grid of
+                // 1/div of the resident slots, for callers that keep several
+                // frames in flight
+                static const int div = [] {
+                        const char *e = std::getenv("VRT_PERSIST_GRID_DIV");
+                        const int v = e ? std::atoi(e) : 1;
+                        return v < 1 ? 1 : v;
+                }();
+                const int full = (p.sc.persist_blocks / div) & ~7;
+                const int cap = std::max(8, p.nranks > 1 ? full - kCollectiveReserve : full);
                 const int g = std::min(cap, need);
                 if (kind == kRenderPersistFast) {
                         hipLaunchKernelGGL(k_render_p<true>, dim3(g), dim3(kPersistBlock), 0, st, p);
