@@ -351,6 +351,8 @@ def main():
     if a.mode == "secondary" and a.frames_in_flight_secondary is not None:
         nfl = max(1, a.frames_in_flight_secondary)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nfl - 1)]
+    if a.mode == "primary":
+        tree.set_frames_in_flight(nfl)  # half-chip persistent grids when frames overlap
     tpr = vrt.tiles_per_rank(film, nshare)
     secondary = a.mode == "secondary"
     img_shape = (a.height, a.width) if secondary else (a.height, a.width, 3)
@@ -517,6 +519,7 @@ def main():
     d9 = None
     if world == 1 and not rehearse and not secondary and not trace and not a.no_d9:
         tree9 = vrt.VoxelOctree(sd, a.depth + 1, device=local)
+        tree9.set_frames_in_flight(nfl)
         img9 = [torch.zeros_like(img) for _ in range(nfl)]
         for k in range(a.warmup):
             tree9.render_tiles_device(cams[k % a.poses], film, 0, 1, 1, img9[k % nfl].data_ptr(),

@@ -176,6 +176,12 @@ int vrt_render(vrt_scene *s, const vrt_camera *cam, const vrt_film *film,
  * vrt_tiles_per_rank()*192 floats (the largest share).  rank=0, nranks=1
  * with image_layout=1 writes the nx*ny*3 image directly instead. */
 int vrt_tiles_per_rank(const vrt_film *film, int nranks);
+/* Launch hint: the caller keeps `n` frames in flight on different streams
+ * (n >= 2) or renders one at a time (n = 1, the default).  With n >= 2 a
+ * persistent render grid takes half of the resident workgroup slots, so
+ * consecutive frames share the chip and one frame's latency-bound ramp-down
+ * runs beside the next frame; results are identical either way. */
+int vrt_scene_set_frames_in_flight(vrt_scene *s, int n);
 int vrt_tile_deal_block(void);
 /* The deal as tables (host, no device): for every tile ty*ntx+tx, its rank
  * and its index k in that rank's buffer. */

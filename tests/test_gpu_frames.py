@@ -157,6 +157,40 @@ def test_two_streams_share_one_scene(proxy):
     assert np.array_equal(bits(a), bits(want[0]))
 
 
+def test_frames_in_flight_match_oracle(proxy):
+    """bench.py's schedule: 3 frames in flight on 3 streams with the
+    half-chip grid hint (vrt_scene_set_frames_in_flight), 1080p frames of 3
+    poses and 8-rank shares of a 4th -- every frame equals the oracle's
+    image of its pose; the hint is then reset."""
+    import torch
+    tree, osc = scenes(proxy, 8)
+    mn, mx = tree.root_box
+    film = vrt.Film(1, 1, 1920, 1080)
+    poses = [vrt.sweep_pose(mn, mx, i, 16) for i in (2, 7, 12, 15)]
+    want = [osc.render(po.camera(*p), 1.0, 1.0, 1920, 1080, nthreads=NTH, samples=False) for p in poses]
+    tree.set_frames_in_flight(3)
+    try:
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        outs = [torch.zeros((1080, 1920, 3), dtype=torch.float32, device="cuda:0") for _ in range(9)]
+        for k in range(9):
+            tree.render_tiles_device(vrt.Camera(*poses[k % 3]), film, 0, 1, 1, outs[k].data_ptr(),
+                                     streams[k % 3].cuda_stream)
+        # 8 ranks' shares of pose 4 on the 3 streams, reassembled
+        tpr = vrt.tiles_per_rank(film, 8)
+        g = torch.zeros((8, tpr * 192), dtype=torch.float32, device="cuda:0")
+        for r in range(8):
+            tree.render_tiles_device(vrt.Camera(*poses[3]), film, r, 8, 0, g[r].data_ptr(), streams[r % 3].cuda_stream)
+        torch.cuda.synchronize()
+        img = torch.zeros((1080, 1920, 3), dtype=torch.float32, device="cuda:0")
+        vrt.unpack_tiles_device(film, 8, g.data_ptr(), img.data_ptr(), None)
+        torch.cuda.synchronize()
+        for k in range(9):
+            assert np.array_equal(bits(outs[k].cpu().numpy()), bits(want[k % 3])), k
+        assert np.array_equal(bits(img.cpu().numpy()), bits(want[3]))
+    finally:
+        tree.set_frames_in_flight(1)
+
+
 def test_forced_defer_pass_matches_oracle(proxy):
     """The persistent fast-path kernel defers a unit whose rays need the
     exact march (a non-zero denormal direction component); k_render_defer

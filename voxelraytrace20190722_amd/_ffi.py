@@ -105,6 +105,7 @@ SIGNATURES = {
                              C.POINTER(Samples), C.POINTER(Stats)]),
     "vrt_tiles_per_rank": (C.c_int, [C.POINTER(Film), C.c_int]),
     "vrt_tile_deal_block": (C.c_int, []),
+    "vrt_scene_set_frames_in_flight": (C.c_int, [C.c_void_p, C.c_int]),
     "vrt_tile_deal_map": (C.c_int, [C.POINTER(Film), C.c_int, i32p, i32p]),
     "vrt_render_tiles_device": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), C.c_int,
                                           C.c_int, C.c_int, _P, _P]),

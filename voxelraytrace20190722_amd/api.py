@@ -399,6 +399,11 @@ class VoxelOctree:
                                             C.c_void_p(stream_ptr) if stream_ptr else None),
               "vrt_render_tiles_device")
 
+    def set_frames_in_flight(self, n):
+        """Launch hint (vrt_scene_set_frames_in_flight): n >= 2 frames kept
+        in flight on different streams -> half-chip persistent grids."""
+        check(lib().vrt_scene_set_frames_in_flight(self.h, int(n)), "vrt_scene_set_frames_in_flight")
+
     def last_kernel_ms(self):
         ms = C.c_float()
         check(lib().vrt_last_kernel_ms(self.h, C.byref(ms)), "vrt_last_kernel_ms")

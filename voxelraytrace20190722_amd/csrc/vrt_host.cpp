@@ -679,6 +679,7 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         s->d_queue = reinterpret_cast<uint32_t *>(base + off[8]);
         HIPCHK(persistent_blocks(&s->dev.persist_blocks, &s->dev.sec_blocks));
         s->dev.nnodes = (int32_t)s->nodes.size();
+        s->dev.grid_div = 1;
         s->dev.max_depth = s->max_depth;
         s->dev.nmat = (int32_t)s->mats.size();
         s->dev.ntex = (int32_t)s->texs.size();
@@ -922,6 +923,17 @@ extern "C" int vrt_tiles_per_rank(const vrt_film *film, int nranks)
         for (int r = 0; r < nranks; ++r)
                 m = std::max(m, deal_count(d, r));
         return m;
+}
+
+extern "C" int vrt_scene_set_frames_in_flight(vrt_scene *s, int n)
+{
+        if (!s || n < 1)
+                return fail(VRT_E_INVALID, "bad argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        // measured: half the slots per frame with 2-3 frames
+        // in flight; a third is slower
+        s->dev.grid_div = n >= 2 ? 2 : 1;
+        return VRT_OK;
 }
 
 extern "C" int vrt_tile_deal_block(void)

@@ -92,6 +92,8 @@ struct DevScene {
                                  // device (a multiple of 8), 0 = no persistent launches
         int32_t sec_blocks;      // the same for the persistent secondary-ray kernel
         int32_t nnodes;          // node count (LDS node staging reads at most this many)
+        int32_t grid_div;        // persistent render grid = resident slots / grid_div
+                                 // (vrt_scene_set_frames_in_flight)
 };
 
 // Work queue of one persistent launch (k_render_p, k_secondary_p): 8

@@ -25,7 +25,6 @@
 
 #include <algorithm>
 #include <climits>
-#include <cstdlib>
 #include <cmath>
 #include <cstring>
 
@@ -2012,15 +2011,9 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 // 4 units, a multiple of 8 for the XCD map)
                 const int need = (p.tiles_this_rank + 7) & ~7;  // 4 units per tile, 4 waves per block
                 // (kCollectiveReserve: room for the RCCL gather of the previous frame)
-                // VRT_PERSIST_GRID_DIV (tuning knob, read once): a grid of
-                // 1/div of the resident slots, for callers that keep several
-                // frames in flight
-                static const int div = [] {
-                        const char *e = std::getenv("VRT_PERSIST_GRID_DIV");
-                        const int v = e ? std::atoi(e) : 1;
-                        return v < 1 ? 1 : v;
-                }();
-                const int full = (p.sc.persist_blocks / div) & ~7;
+                // a caller with frames in flight (vrt_scene_set_frames_in_flight)
+                // gets 1/grid_div of the resident slots per frame
+                const int full = (p.sc.persist_blocks / std::max(1, p.sc.grid_div)) & ~7;
                 const int cap = std::max(8, p.nranks > 1 ? full - kCollectiveReserve : full);
                 const int g = std::min(cap, need);
                 if (kind == kRenderPersistFast) {
