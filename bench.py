@@ -378,6 +378,7 @@ def main():
     works = [None] * nbuf
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(a.steps)]
+    torch.cuda.synchronize()  # buffers were zeroed on torch's stream; frames run on several
 
     def sl(k):
         """frame k's stream slot and buffer slot"""

@@ -180,7 +180,9 @@ int vrt_tiles_per_rank(const vrt_film *film, int nranks);
  * (n >= 2) or renders one at a time (n = 1, the default).  With n >= 2 a
  * persistent render grid takes half of the resident workgroup slots, so
  * consecutive frames share the chip and one frame's latency-bound ramp-down
- * runs beside the next frame; results are identical either way. */
+ * runs beside the next frame; results are identical either way.  Applies to
+ * the device entry points (vrt_render_tiles_device); the synchronous
+ * vrt_render always uses the whole chip. */
 int vrt_scene_set_frames_in_flight(vrt_scene *s, int n);
 int vrt_tile_deal_block(void);
 /* The deal as tables (host, no device): for every tile ty*ntx+tx, its rank

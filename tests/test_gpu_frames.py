@@ -146,6 +146,7 @@ def test_two_streams_share_one_scene(proxy):
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     n = 20  # > 2 x the ring's 8 slots
     outs = [torch.zeros((200, 320, 3), dtype=torch.float32, device="cuda:0") for _ in range(n)]
+    torch.cuda.synchronize()  # the zero fills ran on torch's stream, the renders use others
     for k in range(n):
         st = streams[k % 2]
         tree.render_tiles_device(vrt.Camera(*poses[k % 2]), film, 0, 1, 1, outs[k].data_ptr(), st.cuda_stream)
@@ -172,12 +173,13 @@ def test_frames_in_flight_match_oracle(proxy):
     try:
         streams = [torch.cuda.Stream() for _ in range(3)]
         outs = [torch.zeros((1080, 1920, 3), dtype=torch.float32, device="cuda:0") for _ in range(9)]
+        tpr = vrt.tiles_per_rank(film, 8)
+        g = torch.zeros((8, tpr * 192), dtype=torch.float32, device="cuda:0")
+        torch.cuda.synchronize()  # the zero fills ran on torch's stream, the renders use others
         for k in range(9):
             tree.render_tiles_device(vrt.Camera(*poses[k % 3]), film, 0, 1, 1, outs[k].data_ptr(),
                                      streams[k % 3].cuda_stream)
         # 8 ranks' shares of pose 4 on the 3 streams, reassembled
-        tpr = vrt.tiles_per_rank(film, 8)
-        g = torch.zeros((8, tpr * 192), dtype=torch.float32, device="cuda:0")
         for r in range(8):
             tree.render_tiles_device(vrt.Camera(*poses[3]), film, r, 8, 0, g[r].data_ptr(), streams[r % 3].cuda_stream)
         torch.cuda.synchronize()

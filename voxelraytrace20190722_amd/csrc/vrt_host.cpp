@@ -1163,6 +1163,7 @@ extern "C" int vrt_render(vrt_scene *s, const vrt_camera *cam,
         HIPCHK(hipMemsetAsync(img.p, 0, npix * 3 * sizeof(float), s->stream));
         RenderParams p;
         fill_render_params(s, cam, film, 0, 1, &p);
+        p.sc.grid_div = 1;  // synchronous: one frame at a time, the whole chip
         p.image_layout = 1;
         p.out = static_cast<float *>(img.p);
         auto alloc_fill = [&](DevBuf &b, size_t bytes, int byte) -> hipError_t {
