@@ -27,14 +27,18 @@ def main():
     # the profiled pass's own kernel time is not in the CSVs: take the clock
     # the bench reported to rebuild it
     child_ms = means["GRBM_GUI_ACTIVE"] / 8 / (r["clock_ghz_profiled"] * 1e9) * 1e3
+    # the per-frame time the bench divided by (frame_ms; the launch span with
+    # one frame in flight, older lines)
+    frame_ms = line.get("frame_ms", line["kernel_ms_mean"])
     again = bench.roofline_from_pmc({"means": means, "child_kernel_ms": child_ms, "dispatch": meta},
-                                    line["kernel_ms_mean"], out_bytes, r.get("reference_equivalent_bytes_per_launch"))
+                                    frame_ms, out_bytes, r.get("reference_equivalent_bytes_per_launch"))
     keys = ("achieved", "peak", "frac", "issue_frac_at_clock", "traffic", "l2_hit", "traffic_over_output")
     check = {k: (r.get(k), again.get(k)) for k in keys}
     check["hbm_frac"] = (r["hbm"]["frac"], again["hbm"]["frac"])
     ok = all(abs((a or 0) - (b or 0)) <= 1e-3 * max(1.0, abs(a or 0)) for a, b in check.values())
     summ = {"bench_json": os.path.basename(bj), "build_id": line.get("build_id"), "kernel": meta.get("kernel"),
             "dispatch": meta, "steps": line["steps"], "kernel_ms_mean": line["kernel_ms_mean"],
+            "frame_ms": frame_ms,
             "pmc_mean_per_dispatch": means, "bench_vs_recomputed": check, "agree": ok}
     json.dump(summ, open(os.path.join(d, "summary.json"), "w"), indent=1)
     print(json.dumps({"agree": ok, **{k: v for k, v in check.items()}}))

@@ -520,6 +520,91 @@ __device__ __forceinline__ bool first_min_takes(bool any, float best, float dept
 // differs, and inv_det = 1.0/det -- side-effect free -- is evaluated only
 // for a triangle that passes every test, so the results are identical.
 // The best hit keeps (float)t; ISect::hit = o + (float)t*d is rebuilt once.
+// One record of ray_march_isect's loop: intersect_triangle3 on the record
+// (q0..q2 = the 48-B RefRec48, or q0 + qd1..qd3 = the RefRec64) and the
+// first-minimum update of the best hit (any, best, best_t, m.tri/u/v).
+template <bool kR64>
+__device__ __forceinline__ void mt_record(const float4 q0, const float4 q1, const float4 q2, const double2 qd1,
+                                          const double2 qd2, const double2 qd3, const RayK &r, bool &any,
+                                          float &best, float &best_t, MarchResult &m)
+{
+        const double v0x = q0.x, v0y = q0.y, v0z = q0.z;
+        const double dx = r.d.x, dy = r.d.y, dz = r.d.z;
+        // edge1 = vert1 - vert0, edge2 = vert2 - vert0 (VRT/raytri.cc:
+        // 209-210): stored in double (RefRec64) or made here in the
+        // register-frugal order edge2, pvec, edge1 (RefRec48)
+        double e2x, e2y, e2z;
+        if (kR64) {
+                e2x = qd2.y, e2y = qd3.x, e2z = qd3.y;
+        } else {
+                e2x = (double)q1.z - v0x, e2y = (double)q1.w - v0y, e2z = (double)q2.x - v0z;
+        }
+        // pvec = dir x edge2
+        const double px = dy * e2z - dz * e2y;
+        const double py = dz * e2x - dx * e2z;
+        const double pz = dx * e2y - dy * e2x;
+        const double e1x = kR64 ? qd1.x : (double)q0.w - v0x;
+        const double e1y = kR64 ? qd1.y : (double)q1.x - v0y;
+        const double e1z = kR64 ? qd2.x : (double)q1.y - v0z;
+        // det
+        const double det = e1x * px + e1y * py + e1z * pz;
+        if (!(det > 0.000001) && !(det < -0.000001))
+                return;  // parallel
+        const double tx = (double)r.o.x - v0x, ty = (double)r.o.y - v0y, tz = (double)r.o.z - v0z;
+        const double uu = tx * px + ty * py + tz * pz;
+        const bool pos = det > 0.000001;
+#ifndef VRT_LEAF_SIGNFOLD
+#define VRT_LEAF_SIGNFOLD 1
+#endif
+#if VRT_LEAF_SIGNFOLD
+        // det < 0 branch folded onto the det > 0 one by negation (exact;
+        // round-to-nearest is symmetric, so -(uu + vv) == (-uu) + (-vv)):
+        // the same accept/reject decisions, without divergent sign branches
+        const double sdet = pos ? det : -det, suu = pos ? uu : -uu;
+        if (suu < 0.0 || suu > sdet)
+                return;
+        const double qx = ty * e1z - tz * e1y;
+        const double qy = tz * e1x - tx * e1z;
+        const double qz = tx * e1y - ty * e1x;
+        const double vv = dx * qx + dy * qy + dz * qz;
+        const double svv = pos ? vv : -vv;
+        if (svv < 0.0 || suu + svv > sdet)
+                return;
+#else
+        if (pos ? (uu < 0.0 || uu > det) : (uu > 0.0 || uu < det))
+                return;
+        const double qx = ty * e1z - tz * e1y;
+        const double qy = tz * e1x - tx * e1z;
+        const double qz = tx * e1y - ty * e1x;
+        const double vv = dx * qx + dy * qy + dz * qz;
+        if (pos ? (vv < 0.0 || uu + vv > det) : (vv > 0.0 || uu + vv < det))
+                return;
+#endif
+        const double inv_det = 1.0 / det;
+        const double t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
+        // Triangle::isect (VRT/voxel_octree.cc:449-454)
+        const float fu = clampf((float)(uu * inv_det), 0, 1);
+        const float fv = clampf((float)(vv * inv_det), 0, 1);
+        const float tf = (float)t;
+        const f3 hp = r.o + r.d * tf;
+        const float depth = length(hp - r.o);
+        if (first_min_takes(any, best, depth)) {
+                any = true;
+                best = depth;
+                best_t = tf;
+                m.tri = __float_as_uint(kR64 ? q0.w : q2.y);
+                m.u = fu;
+                m.v = fv;
+        }
+}
+
+// ray_march_isect (VRT/voxel_octree.cc:99-129) over one leaf's records, with
+// intersect_triangle3 (VRT/raytri.cc:197-249) inlined in a register-frugal
+// order.  Every value is the same IEEE double operation on the same
+// operands as mt_isect(); only the evaluation order of independent terms
+// differs, and inv_det = 1.0/det -- side-effect free -- is evaluated only
+// for a triangle that passes every test, so the results are identical.
+// The best hit keeps (float)t; ISect::hit = o + (float)t*d is rebuilt once.
 template <bool kCount, bool kR64>
 __device__ __forceinline__ bool leaf_isect_v2(const void *__restrict__ refs,
                                               uint32_t first, uint32_t n,
@@ -534,89 +619,62 @@ __device__ __forceinline__ bool leaf_isect_v2(const void *__restrict__ refs,
         for (uint32_t k = 0; k < n; ++k) {
                 const float4 *q = kR64 ? reinterpret_cast<const float4 *>(static_cast<const RefRec64 *>(refs) + first + k)
                                        : reinterpret_cast<const float4 *>(static_cast<const RefRec48 *>(refs) + first + k);
-                const float4 q0 = q[0];
-                const double v0x = q0.x, v0y = q0.y, v0z = q0.z;
-                const double dx = r.d.x, dy = r.d.y, dz = r.d.z;
-                // edge1 = vert1 - vert0, edge2 = vert2 - vert0 (VRT/raytri.cc:
-                // 209-210): stored in double (RefRec64) or made here in the
-                // register-frugal order edge2, pvec, edge1 (RefRec48)
                 const double2 *qd = reinterpret_cast<const double2 *>(q);
-                float4 q1, q2;
-                double2 qd1, qd2, qd3;
-                double e2x, e2y, e2z;
+                const float4 q0 = q[0];
+                float4 q1 = q0, q2 = q0;
+                double2 qd1 = {}, qd2 = {}, qd3 = {};
                 if (kR64) {
                         qd1 = qd[1];
                         qd2 = qd[2];
                         qd3 = qd[3];
-                        e2x = qd2.y, e2y = qd3.x, e2z = qd3.y;
                 } else {
                         q1 = q[1];
                         q2 = q[2];
-                        e2x = (double)q1.z - v0x, e2y = (double)q1.w - v0y, e2z = (double)q2.x - v0z;
                 }
-                // pvec = dir x edge2
-                const double px = dy * e2z - dz * e2y;
-                const double py = dz * e2x - dx * e2z;
-                const double pz = dx * e2y - dy * e2x;
-                const double e1x = kR64 ? qd1.x : (double)q0.w - v0x;
-                const double e1y = kR64 ? qd1.y : (double)q1.x - v0y;
-                const double e1z = kR64 ? qd2.x : (double)q1.y - v0z;
-                // det
-                const double det = e1x * px + e1y * py + e1z * pz;
-                if (!(det > 0.000001) && !(det < -0.000001))
-                        continue;  // parallel
-                const double tx = (double)r.o.x - v0x, ty = (double)r.o.y - v0y, tz = (double)r.o.z - v0z;
-                const double uu = tx * px + ty * py + tz * pz;
-                const bool pos = det > 0.000001;
-#ifndef VRT_LEAF_SIGNFOLD
-#define VRT_LEAF_SIGNFOLD 1
-#endif
-#if VRT_LEAF_SIGNFOLD
-                // det < 0 branch folded onto the det > 0 one by negation
-                // (exact; round-to-nearest is symmetric, so -(uu + vv) ==
-                // (-uu) + (-vv)): the same accept/reject decisions, without
-                // divergent sign branches
-                const double sdet = pos ? det : -det, suu = pos ? uu : -uu;
-                if (suu < 0.0 || suu > sdet)
-                        continue;
-                const double qx = ty * e1z - tz * e1y;
-                const double qy = tz * e1x - tx * e1z;
-                const double qz = tx * e1y - ty * e1x;
-                const double vv = dx * qx + dy * qy + dz * qz;
-                const double svv = pos ? vv : -vv;
-                if (svv < 0.0 || suu + svv > sdet)
-                        continue;
-#else
-                if (pos ? (uu < 0.0 || uu > det) : (uu > 0.0 || uu < det))
-                        continue;
-                const double qx = ty * e1z - tz * e1y;
-                const double qy = tz * e1x - tx * e1z;
-                const double qz = tx * e1y - ty * e1x;
-                const double vv = dx * qx + dy * qy + dz * qz;
-                if (pos ? (vv < 0.0 || uu + vv > det) : (vv > 0.0 || uu + vv < det))
-                        continue;
-#endif
-                const double inv_det = 1.0 / det;
-                const double t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
-                // Triangle::isect (VRT/voxel_octree.cc:449-454)
-                const float fu = clampf((float)(uu * inv_det), 0, 1);
-                const float fv = clampf((float)(vv * inv_det), 0, 1);
-                const float tf = (float)t;
-                const f3 hp = r.o + r.d * tf;
-                const float depth = length(hp - r.o);
-                if (first_min_takes(any, best, depth)) {
-                        any = true;
-                        best = depth;
-                        best_t = tf;
-                        m.tri = __float_as_uint(kR64 ? q0.w : q2.y);
-                        m.u = fu;
-                        m.v = fv;
-                }
+                mt_record<kR64>(q0, q1, q2, qd1, qd2, qd3, r, any, best, best_t, m);
         }
         if (any)
                 m.hp = r.o + r.d * best_t;
         if (kCount)
                 m.T += n;
+        return any;
+}
+
+// The same over RefRec48 records, each lane's next record staged one ahead
+// through LDS by LDS-DMA (global_load_lds_dwordx4 x 3: no VGPRs hold it in
+// flight), so a record's load overlaps the previous record's fp64 test.
+// pf = this wave's 3 x 64 float4 LDS block (record bytes 0-15 / 16-31 /
+// 32-47 of lane l at pf[l], pf[64 + l], pf[128 + l]).
+__device__ __forceinline__ void lds_dma16(const void *g, float4 *lds)
+{
+        __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
+__device__ __forceinline__ bool leaf_isect_pf(const RefRec48 *__restrict__ refs, uint32_t first, uint32_t n,
+                                              const RayK &r, MarchResult &m, float4 *pf)
+{
+        bool any = false;
+        float best = 0.f, best_t = 0.f;
+        int lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        auto issue = [&](uint32_t k) {
+                const float4 *g = reinterpret_cast<const float4 *>(refs + first + k);
+                lds_dma16(g, pf);
+                lds_dma16(g + 1, pf + 64);
+                lds_dma16(g + 2, pf + 128);
+        };
+        if (n)
+                issue(0);
+        for (uint32_t k = 0; k < n; ++k) {
+                const float4 q0 = pf[lane], q1 = pf[64 + lane], q2 = pf[128 + lane];
+                // the reads have returned before the next record overwrites them
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (k + 1 < n)
+                        issue(k + 1);
+                const double2 z = {};
+                mt_record<false>(q0, q1, q2, z, z, z, r, any, best, best_t, m);
+        }
+        if (any)
+                m.hp = r.o + r.d * best_t;
         return any;
 }
 
@@ -644,12 +702,14 @@ __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, u
 
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).
-template <bool kCount, bool kFast, int kS, int kStd, bool kUni, bool kR64, int kNS = 0>
+// kPf (RefRec48 scenes): the leaf records come through leaf_isect_pf's LDS
+// prefetch, pf = this wave's LDS block.
+template <bool kCount, bool kFast, int kS, int kStd, bool kUni, bool kR64, int kNS = 0, bool kPf = false>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint2 *stk,
                                           uint32_t *stk_aux,
                                           uint32_t *path_rem,
-                                          MarchResult &m)
+                                          MarchResult &m, float4 *pf = nullptr)
 {
         m.hit = false;
         m.A = 1;
@@ -771,7 +831,11 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 ++d_lp;
                 d_tri += nref;
 #endif
-                const bool lh = leaf_isect<kCount, kUni, kR64>(sc, b, nref, r, m);
+                bool lh;
+                if (kPf && !kR64 && !kCount)
+                        lh = leaf_isect_pf(static_cast<const RefRec48 *>(sc.refs), b, nref, r, m, pf);
+                else
+                        lh = leaf_isect<kCount, kUni, kR64>(sc, b, nref, r, m);
 #if VRT_PHASE_STAMPS
                 d_tleaf += __builtin_amdgcn_s_memtime() - d_t1;
 #endif
@@ -1235,9 +1299,10 @@ constexpr int kRenderBlock = 64 * VRT_RENDER_WAVES;
 // standard-range instantiation is compiled in (fewer live registers); a wave
 // whose rays need another path returns false before writing anything and the
 // caller defers the unit to k_render_defer.
-template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kNS = 0>
+template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kNS = 0,
+          bool kPf = false>
 __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wave, int lane, uint2 *stk,
-                                            uint32_t *stk_aux, uint32_t *path_rem)
+                                            uint32_t *stk_aux, uint32_t *path_rem, float4 *pf = nullptr)
 {
         // the lane id is re-read per unit (volatile asm: not hoisted out of
         // a persistent loop), so its derived per-lane constants are
@@ -1271,7 +1336,7 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         if (kFastOnly) {
                 if (!wave_fast_std(p.sc, r) || (p.test_flags & VRT_TEST_FORCE_DEFER))
                         return false;
-                ray_march<false, true, kS, kFastStd, true, kR64, kNS>(p.sc, r, stk, nullptr, nullptr, m);
+                ray_march<false, true, kS, kFastStd, true, kR64, kNS, kPf>(p.sc, r, stk, nullptr, nullptr, m, pf);
         } else {
                 ray_march_dispatch<kCount, kS, true, kR64, kNS>(p.sc, r, stk, stk_aux, path_rem, m);
         }
@@ -1420,13 +1485,20 @@ constexpr int kCollectiveReserve = 32;
 #ifndef VRT_LDS_NODES
 #define VRT_LDS_NODES 0
 #endif
+#ifndef VRT_LEAF_PF
+#define VRT_LEAF_PF 0
+#endif
 template <bool kFastOnly>
 __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_render_p(RenderParams p)
 {
         constexpr int kNS = kFastOnly ? VRT_LDS_NODES : 0;
         __shared__ uint2 stk[kStack * kPersistBlock];
+        // leaf-record prefetch blocks, 3 KB per wave (VRT_LEAF_PF)
+        constexpr bool kPf = kFastOnly && VRT_LEAF_PF;
+        __shared__ float4 pfbuf[kPf ? 3 * kPersistBlock : 1];
         stage_nodes<kNS>(p.sc.nodes, p.sc.nnodes);
         const int tid = threadIdx.x, lane = tid & 63;
+        float4 *const pf = pfbuf + (kPf ? (tid >> 6) * 192 : 0);
         const UnitMap um = unit_map(p.ntx, p.nty, p.nranks, p.tiles_this_rank, 2);
         const int xcd = blockIdx.x & 7;
         for (int j = 0; j < (VRT_PERSIST_HELP ? 8 : 1); ++j) {
@@ -1443,8 +1515,8 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
 #if VRT_PHASE_STAMPS
                         const unsigned long long d_u0 = __builtin_amdgcn_s_memtime();
 #endif
-                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kNS>(
-                                p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr);
+                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kNS, kPf>(
+                                p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr, pf);
 #if VRT_PHASE_STAMPS
                         if (lane == 0)
                                 atomicAdd(&g_phase[10], __builtin_amdgcn_s_memtime() - d_u0);
