@@ -185,6 +185,11 @@ __host__ __device__ inline int deal_count(const TileDeal &d, int r)
 // rank r's k-th tile -> (tx, ty)
 __host__ __device__ inline void deal_tile(const TileDeal &d, int r, int k, int &tx, int &ty)
 {
+        if (d.nranks == 1) {  // raster order (the general form with G = 1, fewer divisions)
+                tx = k % d.ntx;
+                ty = k / d.ntx;
+                return;
+        }
         const int G2 = d.G * d.G, nb = deal_blocks(d, r);
         if (k < nb * G2) {
                 const int j = r + (k / G2) * d.nranks, w = k % G2;

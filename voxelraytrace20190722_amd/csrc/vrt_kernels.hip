@@ -640,44 +640,6 @@ __device__ __forceinline__ bool leaf_isect_v2(const void *__restrict__ refs,
         return any;
 }
 
-// The same over RefRec48 records, each lane's next record staged one ahead
-// through LDS by LDS-DMA (global_load_lds_dwordx4 x 3: no VGPRs hold it in
-// flight), so a record's load overlaps the previous record's fp64 test.
-// pf = this wave's 3 x 64 float4 LDS block (record bytes 0-15 / 16-31 /
-// 32-47 of lane l at pf[l], pf[64 + l], pf[128 + l]).
-__device__ __forceinline__ void lds_dma16(const void *g, float4 *lds)
-{
-        __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
-}
-__device__ __forceinline__ bool leaf_isect_pf(const RefRec48 *__restrict__ refs, uint32_t first, uint32_t n,
-                                              const RayK &r, MarchResult &m, float4 *pf)
-{
-        bool any = false;
-        float best = 0.f, best_t = 0.f;
-        int lane;
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-        auto issue = [&](uint32_t k) {
-                const float4 *g = reinterpret_cast<const float4 *>(refs + first + k);
-                lds_dma16(g, pf);
-                lds_dma16(g + 1, pf + 64);
-                lds_dma16(g + 2, pf + 128);
-        };
-        if (n)
-                issue(0);
-        for (uint32_t k = 0; k < n; ++k) {
-                const float4 q0 = pf[lane], q1 = pf[64 + lane], q2 = pf[128 + lane];
-                // the reads have returned before the next record overwrites them
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (k + 1 < n)
-                        issue(k + 1);
-                const double2 z = {};
-                mt_record<false>(q0, q1, q2, z, z, z, r, any, best, best_t, m);
-        }
-        if (any)
-                m.hp = r.o + r.d * best_t;
-        return any;
-}
-
 template <bool kCount, bool kUni, bool kR64>
 __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, uint32_t n,
                                            const RayK &r, MarchResult &m)
@@ -702,14 +664,12 @@ __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, u
 
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).
-// kPf (RefRec48 scenes): the leaf records come through leaf_isect_pf's LDS
-// prefetch, pf = this wave's LDS block.
-template <bool kCount, bool kFast, int kS, int kStd, bool kUni, bool kR64, int kNS = 0, bool kPf = false>
+template <bool kCount, bool kFast, int kS, int kStd, bool kUni, bool kR64, int kNS = 0>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint2 *stk,
                                           uint32_t *stk_aux,
                                           uint32_t *path_rem,
-                                          MarchResult &m, float4 *pf = nullptr)
+                                          MarchResult &m)
 {
         m.hit = false;
         m.A = 1;
@@ -831,11 +791,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 ++d_lp;
                 d_tri += nref;
 #endif
-                bool lh;
-                if (kPf && !kR64 && !kCount)
-                        lh = leaf_isect_pf(static_cast<const RefRec48 *>(sc.refs), b, nref, r, m, pf);
-                else
-                        lh = leaf_isect<kCount, kUni, kR64>(sc, b, nref, r, m);
+                const bool lh = leaf_isect<kCount, kUni, kR64>(sc, b, nref, r, m);
 #if VRT_PHASE_STAMPS
                 d_tleaf += __builtin_amdgcn_s_memtime() - d_t1;
 #endif
@@ -1299,10 +1255,9 @@ constexpr int kRenderBlock = 64 * VRT_RENDER_WAVES;
 // standard-range instantiation is compiled in (fewer live registers); a wave
 // whose rays need another path returns false before writing anything and the
 // caller defers the unit to k_render_defer.
-template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kNS = 0,
-          bool kPf = false>
+template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kNS = 0>
 __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wave, int lane, uint2 *stk,
-                                            uint32_t *stk_aux, uint32_t *path_rem, float4 *pf = nullptr)
+                                            uint32_t *stk_aux, uint32_t *path_rem)
 {
         // the lane id is re-read per unit (volatile asm: not hoisted out of
         // a persistent loop), so its derived per-lane constants are
@@ -1336,7 +1291,7 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         if (kFastOnly) {
                 if (!wave_fast_std(p.sc, r) || (p.test_flags & VRT_TEST_FORCE_DEFER))
                         return false;
-                ray_march<false, true, kS, kFastStd, true, kR64, kNS, kPf>(p.sc, r, stk, nullptr, nullptr, m, pf);
+                ray_march<false, true, kS, kFastStd, true, kR64, kNS>(p.sc, r, stk, nullptr, nullptr, m);
         } else {
                 ray_march_dispatch<kCount, kS, true, kR64, kNS>(p.sc, r, stk, stk_aux, path_rem, m);
         }
@@ -1485,20 +1440,13 @@ constexpr int kCollectiveReserve = 32;
 #ifndef VRT_LDS_NODES
 #define VRT_LDS_NODES 0
 #endif
-#ifndef VRT_LEAF_PF
-#define VRT_LEAF_PF 0
-#endif
 template <bool kFastOnly>
 __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_render_p(RenderParams p)
 {
         constexpr int kNS = kFastOnly ? VRT_LDS_NODES : 0;
         __shared__ uint2 stk[kStack * kPersistBlock];
-        // leaf-record prefetch blocks, 3 KB per wave (VRT_LEAF_PF)
-        constexpr bool kPf = kFastOnly && VRT_LEAF_PF;
-        __shared__ float4 pfbuf[kPf ? 3 * kPersistBlock : 1];
         stage_nodes<kNS>(p.sc.nodes, p.sc.nnodes);
         const int tid = threadIdx.x, lane = tid & 63;
-        float4 *const pf = pfbuf + (kPf ? (tid >> 6) * 192 : 0);
         const UnitMap um = unit_map(p.ntx, p.nty, p.nranks, p.tiles_this_rank, 2);
         const int xcd = blockIdx.x & 7;
         for (int j = 0; j < (VRT_PERSIST_HELP ? 8 : 1); ++j) {
@@ -1515,8 +1463,8 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
 #if VRT_PHASE_STAMPS
                         const unsigned long long d_u0 = __builtin_amdgcn_s_memtime();
 #endif
-                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kNS, kPf>(
-                                p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr, pf);
+                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kNS>(
+                                p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr);
 #if VRT_PHASE_STAMPS
                         if (lane == 0)
                                 atomicAdd(&g_phase[10], __builtin_amdgcn_s_memtime() - d_u0);
