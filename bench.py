@@ -263,6 +263,8 @@ def parse():
     p.add_argument("--frames-in-flight", type=int, default=3,
                    help="consecutive frames on this many HIP streams (own output buffers), so a frame's "
                         "ramp-down overlaps the next frame's launch; 1 = one stream")
+    p.add_argument("--rehearse-render-only", action="store_true",
+                   help="with --rehearse-ranks: time the share's renders alone (no gather, no unpack)")
     p.add_argument("--frames-in-flight-secondary", type=int, default=1,
                    help="frames in flight for --mode secondary (36 ms frames: 2 in flight measured 5%% slower)")
     p.add_argument("--rehearse-ranks", type=int, default=0,
@@ -463,7 +465,9 @@ def main():
         render(cam, rank, nshare, 0, tiles[b].data_ptr(), s)
         if timed:
             ev[k][1].record(s)
-        if a.dist_backend == "nccl":
+        if rehearse and a.rehearse_render_only:
+            pass  # diagnostic: the share's renders alone
+        elif a.dist_backend == "nccl":
             # frame k's gather is queued as soon as its render is: the NCCL
             # stream waits for this render only, so its kernel is ready before
             # the next frame's render and runs beside it
