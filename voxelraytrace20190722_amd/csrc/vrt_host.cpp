@@ -626,6 +626,63 @@ extern "C" int vrt_device_count(int *n)
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// DevScene::mnodes: the nodes with every non-root leaf that holds triangles
+// carrying the union box of its triangles, enlarged by eps = 2^-16 * the
+// root's largest extent and rounded outward to float.  Sets lb_center and
+// lb_reach = 16 * that extent: for a ray origin within lb_reach of the
+// centre (per axis) and a point of a leaf's triangles, every slab distance
+// |p - o| / |d| is below 17 * extent / |d|, the three fp32 roundings of
+// (p - o) * (1/d) move it by less than 3 * 2^-24 * 17 * extent / |d| <
+// eps / |d|, so the fp32 line test on the enlarged box passes whenever the
+// exact line meets the unenlarged one -- and intersect_triangle3 accepts a
+// triangle only where the line meets it (up to its fp64 rounding, far below
+// eps).  VRT_LEAF_BOX=0: mnodes = nodes.
+#ifndef VRT_LEAF_BOX
+#define VRT_LEAF_BOX 1
+#endif
+static std::vector<NodeRec> march_nodes(vrt_scene *s, const vrt_scene_desc *d)
+{
+        std::vector<NodeRec> mn = s->nodes;
+        float ext = 0.f;
+        for (int k = 0; k < 3; ++k) {
+                ext = std::max(ext, s->info.root_max[k] - s->info.root_min[k]);
+                s->dev.lb_center[k] = 0.5f * (s->info.root_min[k] + s->info.root_max[k]);
+        }
+        s->dev.lb_reach = 16.f * ext;
+        if (!VRT_LEAF_BOX || !(ext > 0.f) || !std::isfinite(ext)) {
+                s->dev.lb_reach = -1.f;  // never skip
+                return mn;
+        }
+        const double eps = std::ldexp((double)ext, -16);
+        for (size_t i = 1; i < mn.size(); ++i) {
+                NodeRec &nr = mn[i];
+                if (!(nr.a & kLeafBit))
+                        continue;
+                const uint32_t n = nr.a & ~kLeafBit;
+                if (n == 0)
+                        continue;
+                double lo[3] = { HUGE_VAL, HUGE_VAL, HUGE_VAL }, hi[3] = { -HUGE_VAL, -HUGE_VAL, -HUGE_VAL };
+                for (uint32_t j = 0; j < n; ++j) {
+                        const float *p = d->pos + 9 * (size_t)s->ref_tri[nr.b + j];
+                        for (int v = 0; v < 3; ++v)
+                                for (int k = 0; k < 3; ++k) {
+                                        lo[k] = std::min(lo[k], (double)p[3 * v + k]);
+                                        hi[k] = std::max(hi[k], (double)p[3 * v + k]);
+                                }
+                }
+                for (int k = 0; k < 3; ++k) {
+                        float l = (float)(lo[k] - eps), h = (float)(hi[k] + eps);
+                        if ((double)l > lo[k] - eps)
+                                l = std::nextafter(l, -HUGE_VALF);
+                        if ((double)h < hi[k] + eps)
+                                h = std::nextafter(h, HUGE_VALF);
+                        nr.bmin[k] = l;
+                        nr.bmax[k] = h;
+                }
+        }
+        return mn;
+}
+
 static int upload(vrt_scene *s, const vrt_scene_desc *d)
 {
         int rc = check_device(s->device);
@@ -643,15 +700,15 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         const size_t sz_mats = s->mats.size() * sizeof(MatRec);
         const size_t sz_texs = std::max<size_t>(1, s->texs.size()) * sizeof(TexRec);
         const size_t sz_tex = (size_t)std::max<int64_t>(16, s->tex_bytes);
-        size_t off[10];
+        size_t off[11];
         size_t tot = 0;
-        const size_t sizes[9] = { sz_nodes, sz_vox, sz_refs, sz_pos, sz_attr, sz_mats, sz_texs, sz_tex,
-                                  kQueueSlots * kQueueBytes };
-        for (int i = 0; i < 9; ++i) {
+        const size_t sizes[10] = { sz_nodes, sz_vox, sz_refs, sz_pos, sz_attr, sz_mats, sz_texs, sz_tex,
+                                   kQueueSlots * kQueueBytes, sz_nodes };
+        for (int i = 0; i < 10; ++i) {
                 off[i] = tot;
                 tot += align_up(sizes[i]);
         }
-        off[9] = tot;
+        off[10] = tot;
         HIPCHK(hipMalloc(&s->d_mem, tot));
         char *base = static_cast<char *>(s->d_mem);
         HIPCHK(hipMemset(base + off[8], 0, kQueueSlots * kQueueBytes));
@@ -677,6 +734,12 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         s->dev.texs = reinterpret_cast<const TexRec *>(base + off[6]);
         s->dev.tex_data = reinterpret_cast<const uint8_t *>(base + off[7]);
         s->d_queue = reinterpret_cast<uint32_t *>(base + off[8]);
+        {
+                // the march copy of the nodes (DevScene::mnodes)
+                std::vector<NodeRec> mn = march_nodes(s, d);
+                HIPCHK(hipMemcpy(base + off[9], mn.data(), sz_nodes, hipMemcpyHostToDevice));
+                s->dev.mnodes = reinterpret_cast<const NodeRec *>(base + off[9]);
+        }
         HIPCHK(persistent_blocks(&s->dev.persist_blocks, &s->dev.sec_blocks));
         s->dev.nnodes = (int32_t)s->nodes.size();
         s->dev.grid_div = 1;

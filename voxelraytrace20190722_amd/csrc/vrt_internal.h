@@ -94,6 +94,17 @@ struct DevScene {
         int32_t nnodes;          // node count (LDS node staging reads at most this many)
         int32_t grid_div;        // persistent render grid = resident slots / grid_div
                                  // (vrt_scene_set_frames_in_flight)
+        // March copy of the nodes: identical except that every non-root
+        // leaf holding triangles carries, instead of its voxel box, the
+        // union box of its triangles enlarged by lb_eps (leaf_box_ok).  A
+        // ray whose line misses it cannot pass intersect_triangle3 on any
+        // of them (which accepts a hit at any t), so the fast march skips
+        // the leaf's triangle loop; results are unchanged.  The skip is used
+        // for rays with every |o - lb_center| <= lb_reach, where lb_eps
+        // exceeds the fp32 rounding of the line test.
+        const NodeRec *mnodes;
+        float lb_center[3];
+        float lb_reach;
 };
 
 // Work queue of one persistent launch (k_render_p, k_secondary_p): 8

@@ -662,8 +662,31 @@ __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, u
         return leaf_isect_v2<kCount, kR64>(sc.refs, first, n, r, m);
 }
 
+// Does the ray's whole line (every t, as intersect_triangle3 accepts hits
+// behind the origin) meet the box?  The fast path's slab distances (finite:
+// fin_ok); used on DevScene::mnodes' enlarged triangle boxes of leaves.
+__device__ __forceinline__ bool line_meets_box(const float bmin[3], const float bmax[3], const RayK &r)
+{
+        const float ax = (bmin[0] - r.o.x) * r.dinv.x, bx = (bmax[0] - r.o.x) * r.dinv.x;
+        const float ay = (bmin[1] - r.o.y) * r.dinv.y, by = (bmax[1] - r.o.y) * r.dinv.y;
+        const float az = (bmin[2] - r.o.z) * r.dinv.z, bz = (bmax[2] - r.o.z) * r.dinv.z;
+        float t0, t1;
+        asm("v_max3_f32 %0, %1, %2, %3" : "=v"(t0) : "v"(fminf(ax, bx)), "v"(fminf(ay, by)), "v"(fminf(az, bz)));
+        asm("v_min3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(fmaxf(ax, bx)), "v"(fmaxf(ay, by)), "v"(fmaxf(az, bz)));
+        return t0 <= t1;
+}
+// the ray may skip leaves by their triangle boxes (DevScene::mnodes)
+__device__ __forceinline__ bool leaf_box_ok(const DevScene &sc, const RayK &r)
+{
+        return fabsf(r.o.x - sc.lb_center[0]) <= sc.lb_reach && fabsf(r.o.y - sc.lb_center[1]) <= sc.lb_reach &&
+               fabsf(r.o.z - sc.lb_center[2]) <= sc.lb_reach;
+}
+
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
-// stack columns (stride kBlock).
+// stack columns (stride kBlock).  The finite-slab fast walk (kStd == 2)
+// reads DevScene::mnodes and skips a leaf whose triangles' box the ray's
+// line misses (no triangle of it can pass; the leaf is left as the reference
+// leaves it, with no record).
 template <bool kCount, bool kFast, int kS, int kStd, bool kUni, bool kR64, int kNS = 0>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint2 *stk,
@@ -677,6 +700,9 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         m.T = 0;
         float bmin[3], bmax[3];
         uint32_t a, b;
+        constexpr bool kLB = kFast && kStd == 2 && !kCount;
+        const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
+        const bool lbok = kLB && __all(leaf_box_ok(sc, r));  // wave-uniform: held in SGPRs
         load_node_st<kNS>(sc.nodes, 0, bmin, bmax, a, b);
         if (!aabb_isect(bmin, bmax, r.o, r.dinv, r.tmin, r.tmax))
                 return;
@@ -746,7 +772,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         node = base + ci;
                         if (kCount)
                                 path_rem[depth * kS] = 7u - ((fpos >> (3 * ci)) & 7u);
-                        load_node_st<kNS>(sc.nodes, node, bmin, bmax, a, b);
+                        load_node_st<kNS>(nodes, node, bmin, bmax, a, b);
                         if (!(a & kLeafBit)) {
                                 if (cnt) {
                                         stk[sp * kS] = make_uint2(base, order | ((uint32_t)cnt << 24));
@@ -765,6 +791,8 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         nref = a & ~kLeafBit;
                         if (nref == 0)
                                 continue;  // empty leaf (instrumented walk only)
+                        if (kLB && lbok && !line_meets_box(bmin, bmax, r))
+                                continue;  // no triangle of this leaf can pass
                         leaf = true;
                         break;
                 }
@@ -857,7 +885,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 const uint32_t node = base + ci;
                 if (kCount)
                         path_rem[depth * kS] = 7u - ((fpos >> (3 * ci)) & 7u);
-                load_node_st<kNS>(sc.nodes, node, bmin, bmax, a, b);
+                load_node_st<kNS>(nodes, node, bmin, bmax, a, b);
                 if (!(a & kLeafBit)) {
                         if (cnt) {
                                 stk[sp * kS] = make_uint2(base, order | ((uint32_t)cnt << 24));
@@ -1107,6 +1135,10 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
 {
         float bmin[3], bmax[3];
         uint32_t a, b;
+        // finite-slab walk: leaves skipped by their triangle boxes (as ray_march)
+        constexpr bool kLB = kFast && kFin;
+        const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
+        const bool lbok = kLB && __all(leaf_box_ok(sc, r));  // wave-uniform: held in SGPRs
         load_node(sc.nodes, 0, bmin, bmax, a, b);
         if (!aabb_isect(bmin, bmax, r.o, r.dinv, r.tmin, r.tmax))
                 return false;
@@ -1134,7 +1166,7 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
                         }
                         const uint32_t ci = (uint32_t)__builtin_ctz(mask) ^ s;
                         mask &= mask - 1u;
-                        load_node(sc.nodes, base + ci, bmin, bmax, a, b);
+                        load_node(nodes, base + ci, bmin, bmax, a, b);
                         if (!(a & kLeafBit)) {
                                 if (mask) {
                                         stk[sp * kS] = make_uint2(base, mask);
@@ -1145,6 +1177,8 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
                                 continue;
                         }
                         nref = a & ~kLeafBit;  // > 0: the content mask skips empty leaves
+                        if (kLB && lbok && !line_meets_box(bmin, bmax, r))
+                                continue;  // no triangle of this leaf can pass
                         leaf = true;
                         break;
                 }
@@ -1445,7 +1479,7 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
 {
         constexpr int kNS = kFastOnly ? VRT_LDS_NODES : 0;
         __shared__ uint2 stk[kStack * kPersistBlock];
-        stage_nodes<kNS>(p.sc.nodes, p.sc.nnodes);
+        stage_nodes<kNS>(p.sc.mnodes, p.sc.nnodes);  // = nodes for internal nodes and the root
         const int tid = threadIdx.x, lane = tid & 63;
         const UnitMap um = unit_map(p.ntx, p.nty, p.nranks, p.tiles_this_rank, 2);
         const int xcd = blockIdx.x & 7;
