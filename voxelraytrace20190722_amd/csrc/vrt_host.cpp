@@ -640,9 +640,25 @@ static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 #ifndef VRT_LEAF_BOX
 #define VRT_LEAF_BOX 1
 #endif
-static std::vector<NodeRec> march_nodes(vrt_scene *s, const vrt_scene_desc *d)
+//
+// DevScene::xnodes (VRT_NODE_BOX): every node's own record followed by the
+// union box of all triangles below it (a leaf: its own), enlarged the same
+// way -- the same bound holds, as every such triangle lies in the root box.
+// Nodes with no triangle below them (never visited by the content-masked
+// walk) and every node when the skip is off carry their voxel box.
+static std::vector<NodeRec> march_nodes(vrt_scene *s, const vrt_scene_desc *d, std::vector<XNodeRec> &xn)
 {
         std::vector<NodeRec> mn = s->nodes;
+        const size_t nn = mn.size();
+        xn.resize(nn);
+        for (size_t i = 0; i < nn; ++i) {
+                xn[i] = XNodeRec{};
+                xn[i].n = s->nodes[i];
+                for (int k = 0; k < 3; ++k) {
+                        xn[i].tmin[k] = s->nodes[i].bmin[k];
+                        xn[i].tmax[k] = s->nodes[i].bmax[k];
+                }
+        }
         float ext = 0.f;
         for (int k = 0; k < 3; ++k) {
                 ext = std::max(ext, s->info.root_max[k] - s->info.root_min[k]);
@@ -654,31 +670,53 @@ static std::vector<NodeRec> march_nodes(vrt_scene *s, const vrt_scene_desc *d)
                 return mn;
         }
         const double eps = std::ldexp((double)ext, -16);
-        for (size_t i = 1; i < mn.size(); ++i) {
-                NodeRec &nr = mn[i];
-                if (!(nr.a & kLeafBit))
-                        continue;
-                const uint32_t n = nr.a & ~kLeafBit;
-                if (n == 0)
-                        continue;
-                double lo[3] = { HUGE_VAL, HUGE_VAL, HUGE_VAL }, hi[3] = { -HUGE_VAL, -HUGE_VAL, -HUGE_VAL };
-                for (uint32_t j = 0; j < n; ++j) {
-                        const float *p = d->pos + 9 * (size_t)s->ref_tri[nr.b + j];
-                        for (int v = 0; v < 3; ++v)
+        // unenlarged triangle boxes, bottom-up (children follow their parent
+        // in the BFS array)
+        std::vector<double> lo(3 * nn, HUGE_VAL), hi(3 * nn, -HUGE_VAL);
+        for (size_t i = nn; i-- > 0;) {
+                const NodeRec &nr = s->nodes[i];
+                double *l = &lo[3 * i], *h = &hi[3 * i];
+                if (nr.a & kLeafBit) {
+                        const uint32_t n = nr.a & ~kLeafBit;
+                        for (uint32_t j = 0; j < n; ++j) {
+                                const float *p = d->pos + 9 * (size_t)s->ref_tri[nr.b + j];
+                                for (int v = 0; v < 3; ++v)
+                                        for (int k = 0; k < 3; ++k) {
+                                                l[k] = std::min(l[k], (double)p[3 * v + k]);
+                                                h[k] = std::max(h[k], (double)p[3 * v + k]);
+                                        }
+                        }
+                } else {
+                        for (uint32_t c = 0; c < 8; ++c)
                                 for (int k = 0; k < 3; ++k) {
-                                        lo[k] = std::min(lo[k], (double)p[3 * v + k]);
-                                        hi[k] = std::max(hi[k], (double)p[3 * v + k]);
+                                        l[k] = std::min(l[k], lo[3 * (nr.a + c) + k]);
+                                        h[k] = std::max(h[k], hi[3 * (nr.a + c) + k]);
                                 }
                 }
+        }
+        for (size_t i = 1; i < nn; ++i) {
+                const double *l = &lo[3 * i], *h = &hi[3 * i];
+                if (!(l[0] <= h[0]))
+                        continue;  // no triangle below this node
+                float bl[3], bh[3];
                 for (int k = 0; k < 3; ++k) {
-                        float l = (float)(lo[k] - eps), h = (float)(hi[k] + eps);
-                        if ((double)l > lo[k] - eps)
-                                l = std::nextafter(l, -HUGE_VALF);
-                        if ((double)h < hi[k] + eps)
-                                h = std::nextafter(h, HUGE_VALF);
-                        nr.bmin[k] = l;
-                        nr.bmax[k] = h;
+                        float fl = (float)(l[k] - eps), fh = (float)(h[k] + eps);
+                        if ((double)fl > l[k] - eps)
+                                fl = std::nextafter(fl, -HUGE_VALF);
+                        if ((double)fh < h[k] + eps)
+                                fh = std::nextafter(fh, HUGE_VALF);
+                        bl[k] = fl;
+                        bh[k] = fh;
                 }
+                for (int k = 0; k < 3; ++k) {
+                        xn[i].tmin[k] = bl[k];
+                        xn[i].tmax[k] = bh[k];
+                }
+                if (mn[i].a & kLeafBit)
+                        for (int k = 0; k < 3; ++k) {
+                                mn[i].bmin[k] = bl[k];
+                                mn[i].bmax[k] = bh[k];
+                        }
         }
         return mn;
 }
@@ -700,15 +738,16 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         const size_t sz_mats = s->mats.size() * sizeof(MatRec);
         const size_t sz_texs = std::max<size_t>(1, s->texs.size()) * sizeof(TexRec);
         const size_t sz_tex = (size_t)std::max<int64_t>(16, s->tex_bytes);
-        size_t off[11];
+        size_t off[12];
         size_t tot = 0;
-        const size_t sizes[10] = { sz_nodes, sz_vox, sz_refs, sz_pos, sz_attr, sz_mats, sz_texs, sz_tex,
-                                   kQueueSlots * kQueueBytes, sz_nodes };
-        for (int i = 0; i < 10; ++i) {
+        const size_t sz_xnodes = VRT_NODE_BOX ? s->nodes.size() * sizeof(XNodeRec) : 0;
+        const size_t sizes[11] = { sz_nodes, sz_vox, sz_refs, sz_pos, sz_attr, sz_mats, sz_texs, sz_tex,
+                                   kQueueSlots * kQueueBytes, sz_nodes, sz_xnodes };
+        for (int i = 0; i < 11; ++i) {
                 off[i] = tot;
                 tot += align_up(sizes[i]);
         }
-        off[10] = tot;
+        off[11] = tot;
         HIPCHK(hipMalloc(&s->d_mem, tot));
         char *base = static_cast<char *>(s->d_mem);
         HIPCHK(hipMemset(base + off[8], 0, kQueueSlots * kQueueBytes));
@@ -735,10 +774,14 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         s->dev.tex_data = reinterpret_cast<const uint8_t *>(base + off[7]);
         s->d_queue = reinterpret_cast<uint32_t *>(base + off[8]);
         {
-                // the march copy of the nodes (DevScene::mnodes)
-                std::vector<NodeRec> mn = march_nodes(s, d);
+                // the march copies of the nodes (DevScene::mnodes, xnodes)
+                std::vector<XNodeRec> xn;
+                std::vector<NodeRec> mn = march_nodes(s, d, xn);
                 HIPCHK(hipMemcpy(base + off[9], mn.data(), sz_nodes, hipMemcpyHostToDevice));
                 s->dev.mnodes = reinterpret_cast<const NodeRec *>(base + off[9]);
+                if (sz_xnodes)
+                        HIPCHK(hipMemcpy(base + off[10], xn.data(), sz_xnodes, hipMemcpyHostToDevice));
+                s->dev.xnodes = reinterpret_cast<const XNodeRec *>(base + off[10]);
         }
         HIPCHK(persistent_blocks(&s->dev.persist_blocks, &s->dev.sec_blocks));
         s->dev.nnodes = (int32_t)s->nodes.size();

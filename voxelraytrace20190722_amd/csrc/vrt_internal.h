@@ -26,6 +26,24 @@ struct alignas(16) NodeRec {
 static_assert(sizeof(NodeRec) == 32, "NodeRec must be 32 B");
 constexpr uint32_t kLeafBit = 0x80000000u;
 
+// March record of the node triangle-box walk (DevScene::xnodes): the node's
+// own record (voxel box, a, b) followed by the union box of every triangle
+// below it (a leaf: its own triangles), enlarged by lb_eps -- one 64-B
+// record, so the walk fetches both halves with one address.
+struct alignas(16) XNodeRec {
+        NodeRec n;
+        float tmin[3];
+        float tmax[3];
+        uint32_t pad[2];
+};
+static_assert(sizeof(XNodeRec) == 64, "XNodeRec must be 64 B");
+
+// The node triangle-box skip (internal nodes too, DevScene::xnodes):
+// 1 = the finite-slab walks read xnodes, 0 = mnodes (leaves only).
+#ifndef VRT_NODE_BOX
+#define VRT_NODE_BOX 1
+#endif
+
 // Leaf-list records, in leaf order with the vertices inlined (no dependent
 // index load in the leaf loop).  Two formats, chosen per scene:
 // RefRec48 for small leaves (fewer bytes per gather), RefRec64 for scenes
@@ -103,6 +121,10 @@ struct DevScene {
         // for rays with every |o - lb_center| <= lb_reach, where lb_eps
         // exceeds the fp32 rounding of the line test.
         const NodeRec *mnodes;
+        // The same skip for every node (VRT_NODE_BOX): a subtree whose
+        // triangles' enlarged union box the line misses holds no leaf that
+        // can yield a record, so the walk does not expand it.
+        const XNodeRec *xnodes;
         float lb_center[3];
         float lb_reach;
 };

@@ -57,6 +57,23 @@ __device__ __forceinline__ void load_node(const NodeRec *__restrict__ nodes,
         b = __float_as_uint(q1.w);
 }
 
+// DevScene::xnodes record i: the node record and the triangle box below it
+__device__ __forceinline__ void load_xnode(const XNodeRec *__restrict__ x, uint32_t i, float bmin[3],
+                                           float bmax[3], uint32_t &a, uint32_t &b, float tmn[3], float tmx[3])
+{
+        const float4 *q = reinterpret_cast<const float4 *>(x + i);
+        const float4 q0 = q[0];
+        const float4 q1 = q[1];
+        const float4 q2 = q[2];
+        const float2 q3 = *reinterpret_cast<const float2 *>(q + 3);
+        bmin[0] = q0.x; bmin[1] = q0.y; bmin[2] = q0.z;
+        bmax[0] = q0.w; bmax[1] = q1.x; bmax[2] = q1.y;
+        a = __float_as_uint(q1.z);
+        b = __float_as_uint(q1.w);
+        tmn[0] = q2.x; tmn[1] = q2.y; tmn[2] = q2.z;
+        tmx[0] = q2.w; tmx[1] = q3.x; tmx[2] = q3.y;
+}
+
 // LDS copy of the first kNS node records (the top BFS levels: node 0 is the
 // root, then whole levels in order), staged once per workgroup by
 // stage_nodes(); node i < kNS is read from it, the rest from HBM/L2.
@@ -701,6 +718,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         float bmin[3], bmax[3];
         uint32_t a, b;
         constexpr bool kLB = kFast && kStd == 2 && !kCount;
+        constexpr bool kNB = kLB && VRT_NODE_BOX;  // every visited node by its triangle box
         const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
         const bool lbok = kLB && __all(leaf_box_ok(sc, r));  // wave-uniform: held in SGPRs
         load_node_st<kNS>(sc.nodes, 0, bmin, bmax, a, b);
@@ -772,7 +790,14 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         node = base + ci;
                         if (kCount)
                                 path_rem[depth * kS] = 7u - ((fpos >> (3 * ci)) & 7u);
-                        load_node_st<kNS>(nodes, node, bmin, bmax, a, b);
+                        if (kNB) {
+                                float tmn[3], tmx[3];
+                                load_xnode(sc.xnodes, node, bmin, bmax, a, b, tmn, tmx);
+                                if (lbok && !line_meets_box(tmn, tmx, r))
+                                        continue;  // no triangle below this node can pass
+                        } else {
+                                load_node_st<kNS>(nodes, node, bmin, bmax, a, b);
+                        }
                         if (!(a & kLeafBit)) {
                                 if (cnt) {
                                         stk[sp * kS] = make_uint2(base, order | ((uint32_t)cnt << 24));
@@ -791,7 +816,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         nref = a & ~kLeafBit;
                         if (nref == 0)
                                 continue;  // empty leaf (instrumented walk only)
-                        if (kLB && lbok && !line_meets_box(bmin, bmax, r))
+                        if (kLB && !kNB && lbok && !line_meets_box(bmin, bmax, r))
                                 continue;  // no triangle of this leaf can pass
                         leaf = true;
                         break;
@@ -1137,6 +1162,7 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
         uint32_t a, b;
         // finite-slab walk: leaves skipped by their triangle boxes (as ray_march)
         constexpr bool kLB = kFast && kFin;
+        constexpr bool kNB = kLB && VRT_NODE_BOX;  // every visited node by its triangle box
         const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
         const bool lbok = kLB && __all(leaf_box_ok(sc, r));  // wave-uniform: held in SGPRs
         load_node(sc.nodes, 0, bmin, bmax, a, b);
@@ -1166,7 +1192,14 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
                         }
                         const uint32_t ci = (uint32_t)__builtin_ctz(mask) ^ s;
                         mask &= mask - 1u;
-                        load_node(nodes, base + ci, bmin, bmax, a, b);
+                        if (kNB) {
+                                float tmn[3], tmx[3];
+                                load_xnode(sc.xnodes, base + ci, bmin, bmax, a, b, tmn, tmx);
+                                if (lbok && !line_meets_box(tmn, tmx, r))
+                                        continue;  // no triangle below this node can pass
+                        } else {
+                                load_node(nodes, base + ci, bmin, bmax, a, b);
+                        }
                         if (!(a & kLeafBit)) {
                                 if (mask) {
                                         stk[sp * kS] = make_uint2(base, mask);
@@ -1177,7 +1210,7 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
                                 continue;
                         }
                         nref = a & ~kLeafBit;  // > 0: the content mask skips empty leaves
-                        if (kLB && lbok && !line_meets_box(bmin, bmax, r))
+                        if (kLB && !kNB && lbok && !line_meets_box(bmin, bmax, r))
                                 continue;  // no triangle of this leaf can pass
                         leaf = true;
                         break;
