@@ -71,7 +71,7 @@ variant: $(HOSTOBJS) $(BLD)/vrt_build.o | $(BLD)
 	mkdir -p build/variants
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
-	  build/variants/k_$(NAME).o $(BLD)/vrt_build.o $(HOSTOBJS) -lpthread
+	  build/variants/k_$(NAME).o $(BLD)/vrt_build.o $(HOSTOBJS) $(BLD)/vrt_build_id.o -lpthread
 
 # variant that also rebuilds the host side (for data-layout changes)
 fullvariant: $(BLD)/vrt_build.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o | $(BLD)
@@ -80,7 +80,7 @@ fullvariant: $(BLD)/vrt_build.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_o
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_host.cpp -o build/variants/h_$(NAME).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
 	  build/variants/k_$(NAME).o build/variants/h_$(NAME).o $(BLD)/vrt_build.o \
-	  $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o -lpthread
+	  $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o $(BLD)/vrt_build_id.o -lpthread
 
 # ISA listing + register/occupancy report of the kernels (for DESIGN.md)
 isa: | $(BLD)
