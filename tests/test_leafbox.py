@@ -6,7 +6,10 @@ line passes closest to the box faces) from origins up to lb_reach = 16 x
 the scene extent away, the leaf box as tight as it gets (one triangle), the
 device's fp32 line test restated op for op in numpy float32, and the
 reference's own fp64 Moller-Trumbore (the library's intersect_triangle3
-export, bit-exact to VRT/raytri.cc) as the judge of acceptance."""
+export, bit-exact to VRT/raytri.cc) as the judge of acceptance.  The node
+triangle-box skip (DevScene::xnodes) tests unions of such boxes with the same
+enlargement and the same line test: a union contains each triangle's box,
+so a line this test keeps for one triangle is kept for every node above it."""
 import numpy as np
 
 import voxelraytrace20190722_amd as vrt
