@@ -203,21 +203,23 @@ def test_ray_march_extreme_rays_match_oracle(proxy_small, depth):
     assert _same_f32(g["normal"], o["normal"])
 
 
-@pytest.mark.parametrize("nranks", [2, 3, 8])
-def test_tile_partition_reassembles_image(proxy_small, nranks):
-    """Per-rank tile renders + rank-major gather + unpack == one image render."""
+@pytest.mark.parametrize("nranks,nx,ny", [(2, 200, 120), (3, 200, 120), (8, 200, 120), (3, 204, 122)])
+def test_tile_partition_reassembles_image(proxy_small, nranks, nx, ny):
+    """Per-rank tile renders + rank-major gather + unpack == one image render
+    (sides that are multiples of 8: the 16-B chunk unpack k_unpack4; 204 x
+    122: the per-pixel k_unpack, pixels outside the 8 * (n/8) area zero)."""
     import torch
     tree = vrt.VoxelOctree(proxy_small, 7)
     mn, mx = tree.root_box
     fov, eye, spot, up = vrt.sweep_pose(mn, mx, 2, 16)
     cam = vrt.Camera(fov, eye, spot, up)
-    film = vrt.Film(1, 1, 200, 120)  # 25 x 15 tiles
+    film = vrt.Film(1, 1, nx, ny)  # 25 x 15 tiles
     tpr = vrt.tiles_per_rank(film, nranks)
     dev = torch.device("cuda:0")
     gathered = torch.zeros((nranks, tpr * 192), dtype=torch.float32, device=dev)
     for r in range(nranks):
         tree.render_tiles_device(cam, film, r, nranks, 0, gathered[r].data_ptr(), None)
-    img = torch.zeros((120, 200, 3), dtype=torch.float32, device=dev)
+    img = torch.full((ny, nx, 3), 7.0, dtype=torch.float32, device=dev)
     vrt.unpack_tiles_device(film, nranks, gathered.data_ptr(), img.data_ptr(), None)
     torch.cuda.synchronize()
     direct = tree.render(cam, film)
@@ -227,7 +229,7 @@ def test_tile_partition_reassembles_image(proxy_small, nranks):
     g = gathered.cpu().numpy()
     for r in range(nranks):
         assert np.array_equal(bits(g[r]), bits(vd.pack_tiles_host(direct, r, nranks)))
-    assert np.array_equal(bits(vd.unpack_tiles_host(g, 200, 120, nranks)), bits(direct))
+    assert np.array_equal(bits(vd.unpack_tiles_host(g, nx, ny, nranks)), bits(direct))
 
 
 def test_full_size_frame_properties():
