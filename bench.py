@@ -189,6 +189,14 @@ def roofline_from_pmc(pmc, kernel_ms, out_bytes, ref_bytes):
         "valu_instr_per_wave": round(m["SQ_INSTS_VALU"] / max(1.0, m["SQ_WAVES"]), 1),
         "avg_waves_per_cu": round(4 * m["SQ_WAVE_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8) / N_CU, 2),
         "reference_equivalent_bytes_per_launch": ref_bytes,
+        # which launch time `achieved` divides by: with frames in flight
+        # launches overlap (the HIP-event span of one launch and rocprofv3's
+        # kernel duration then cover 2-3 frames), so the per-launch time is
+        # the step time; single_launch_ms is one launch alone (the PMC
+        # passes run one frame in flight, as the 1-frame kernel trace)
+        "time_basis": {"launch_ms": round(kernel_ms, 4), "single_launch_ms": round(cms, 4),
+                       "achieved_single_launch": round(m["SQ_INSTS_VALU"] / (cms * 1e-3) / 1e9, 1),
+                       "frac_single_launch": round(m["SQ_INSTS_VALU"] / (cms * 1e-3) / 1e9 / peak, 4)},
         "kernel": pmc["dispatch"].get("kernel"),
         "dispatch": pmc["dispatch"],
         "source": "live rocprofv3 --pmc passes of this bench command (counters per timed dispatch)",
