@@ -152,7 +152,7 @@ def run_pmc(a, kernel_prefix, save_dir=""):
     return {"means": means, "child_kernel_ms": child_ms.get("sq"), "dispatch": meta}, None
 
 
-def roofline_from_pmc(pmc, kernel_ms, out_bytes, ref_bytes):
+def roofline_from_pmc(pmc, kernel_ms, out_bytes, ref_bytes, single_ms=None):
     """The measured roofline of the dominant kernel: VALU issue (the limiter,
     DESIGN.md §4) -- the VALU wave-instructions of one launch (SQ_INSTS_VALU)
     over this run's per-frame device time (frame_ms), against the issue peak at the max
@@ -192,11 +192,14 @@ def roofline_from_pmc(pmc, kernel_ms, out_bytes, ref_bytes):
         # which launch time `achieved` divides by: with frames in flight
         # launches overlap (the HIP-event span of one launch and rocprofv3's
         # kernel duration then cover 2-3 frames), so the per-launch time is
-        # the step time; single_launch_ms is one launch alone (the PMC
-        # passes run one frame in flight, as the 1-frame kernel trace)
-        "time_basis": {"launch_ms": round(kernel_ms, 4), "single_launch_ms": round(cms, 4),
-                       "achieved_single_launch": round(m["SQ_INSTS_VALU"] / (cms * 1e-3) / 1e9, 1),
-                       "frac_single_launch": round(m["SQ_INSTS_VALU"] / (cms * 1e-3) / 1e9 / peak, 4)},
+        # the step time; single_launch_ms is one launch alone (the same
+        # frames, one in flight, HIP events in this process: what the
+        # one-frame rocprofv3 kernel trace shows)
+        "time_basis": {"launch_ms": round(kernel_ms, 4), "single_launch_ms": round(single_ms or kernel_ms, 4),
+                       "achieved_single_launch": round(m["SQ_INSTS_VALU"] / ((single_ms or kernel_ms) * 1e-3) / 1e9,
+                                                       1),
+                       "frac_single_launch": round(m["SQ_INSTS_VALU"] / ((single_ms or kernel_ms) * 1e-3) / 1e9
+                                                   / peak, 4)},
         "kernel": pmc["dispatch"].get("kernel"),
         "dispatch": pmc["dispatch"],
         "source": "live rocprofv3 --pmc passes of this bench command (counters per timed dispatch)",
@@ -574,6 +577,23 @@ def main():
                     "note": "vrt_render into a host float RGB array (24.9 MB at 1080p over PCIe per frame), "
                             "device buffers allocated per call"}
 
+    # one launch alone: the same frames with one frame in flight (the
+    # roofline's time_basis; equal to frame_ms when nfl == 1)
+    single_ms = frame_ms
+    if world == 1 and not rehearse and not secondary and not trace and nfl > 1 and not a.no_pmc:
+        tree.set_frames_in_flight(1)
+        for k in range(2):
+            render(cams[k % a.poses], 0, 1, 1, imgs[0].data_ptr(), stream)
+        ev1 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+        torch.cuda.synchronize()
+        for k in range(a.steps):
+            ev1[k][0].record(stream)
+            render(cams[k % a.poses], 0, 1, 1, imgs[0].data_ptr(), stream)
+            ev1[k][1].record(stream)
+        torch.cuda.synchronize()
+        single_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in ev1]))
+        tree.set_frames_in_flight(nfl)
+
     roof = None
     ref_bytes, per_ray = None, None
     if not a.no_counters and not rehearse and not secondary and not trace:
@@ -607,7 +627,7 @@ def main():
         pmc, why = run_pmc(a, "k_secondary" if secondary else "k_render", a.pmc_save)
         out_bytes = (W8 * H8 * 4) if secondary else (W8 * H8 * 12 // nshare)
         if pmc:
-            roof = roofline_from_pmc(pmc, frame_ms, out_bytes, ref_bytes)
+            roof = roofline_from_pmc(pmc, frame_ms, out_bytes, ref_bytes, single_ms)
             if per_ray:
                 roof["per_ray"] = per_ray
             roof["build_id"] = vrt.build_id()
