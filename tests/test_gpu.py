@@ -532,3 +532,39 @@ def test_device_build_edge_scenes():
                 assert np.array_equal(bits(x), bits(y))
             for x, y in zip(h.leaves(), g.leaves()):
                 assert np.array_equal(x, y)
+
+
+def _small_soup(n=1500, seed=11):
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-1, 1, (n, 1, 3))
+    pos = (c + rng.normal(0, 0.05, (n, 3, 3))).astype(np.float32).reshape(n, 9)
+    nrm = rng.normal(0, 1, (n, 9)).astype(np.float32)
+    return vrt.SceneData(pos, nrm)
+
+
+@pytest.mark.parametrize("depth", [10, 11])
+def test_maximum_depth_matches_oracle(depth):
+    """max_depth up to VRT_MAX_DEPTH (11: voxel ids pack 10 bits per axis;
+    the LDS stack holds max_depth - 2 live entries): a soup of small
+    triangles at the finest grids -- camera renders (per-sample ids, counters,
+    RGB bits) and batched arbitrary rays against the oracle."""
+    sd = _small_soup()
+    tree = vrt.VoxelOctree(sd, depth)
+    osc = po.Scene(sd, depth)
+    mn, mx = tree.root_box
+    for pose in (3, 11):
+        fov, eye, spot, up = vrt.sweep_pose(mn, mx, pose, 16)
+        rgb, so = tree.render(vrt.Camera(fov, eye, spot, up), vrt.Film(1, 1, 48, 48), samples=True,
+                              counters=True)
+        orgb, oso = osc.render(po.camera(fov, eye, spot, up), 1.0, 1.0, 48, 48, film_index=1, nthreads=8)
+        assert so["hit"].sum() > 1000, pose
+        for key in ("hit", "tri", "voxel", "counters"):
+            assert np.array_equal(so[key], oso[key]), (depth, pose, key)
+        assert np.array_equal(bits(rgb), bits(orgb)), (depth, pose)
+    rays = _random_rays(np.random.default_rng(depth), 4000, mn, mx)
+    g = tree.ray_march(rays)
+    o = osc.ray_march(rays)
+    assert o["hit"].sum() > 300
+    for key in ("hit", "tri", "voxel"):
+        assert np.array_equal(g[key], o[key]), key
+    assert np.array_equal(bits(g["hit_p"]), bits(o["hit_p"]))
