@@ -274,6 +274,9 @@ def parse():
     p.add_argument("--frames-in-flight", type=int, default=3,
                    help="consecutive frames on this many HIP streams (own output buffers), so a frame's "
                         "ramp-down overlaps the next frame's launch; 1 = one stream")
+    p.add_argument("--rehearse-rank", type=int, default=0,
+                   help="with --rehearse-ranks: whose share to render (0: rank 0, which also gathers and "
+                        "unpacks; from 4 ranks on the deal gives it fewer tiles than the others)")
     p.add_argument("--rehearse-render-only", action="store_true",
                    help="with --rehearse-ranks: time the share's renders alone (no gather, no unpack)")
     p.add_argument("--frames-in-flight-secondary", type=int, default=1,
@@ -473,7 +476,7 @@ def main():
                 ev[k][1].record(s)
             return
         finish(b, s)  # frame k - nbuf used this buffer pair (normally finished already)
-        render(cam, rank, nshare, 0, tiles[b].data_ptr(), s)
+        render(cam, a.rehearse_rank if rehearse else rank, nshare, 0, tiles[b].data_ptr(), s)
         if timed:
             ev[k][1].record(s)
         if rehearse and a.rehearse_render_only:
@@ -783,9 +786,10 @@ def main():
             # the RCCL call sequence, on one GPU; the xGMI transfer is absent
             out["metric"] = "rehearsal: " + metric
             out["value"] = None
-            out["config"]["parallelism"] = f"rank 0 of {nshare} screen-tile shares + rccl gather (1-rank group)"
+            out["config"]["parallelism"] = (f"rank {a.rehearse_rank}'s share of {nshare} screen-tile shares + "
+                                            f"rccl gather (1-rank group)")
             out["rehearsal"] = {
-                "ranks": nshare, "frames_per_s": round(a.steps / elapsed, 2),
+                "ranks": nshare, "share_of_rank": a.rehearse_rank, "frames_per_s": round(a.steps / elapsed, 2),
                 "projected_Mrays_per_s_without_xgmi": round(value, 2),
                 "share_kernel_ms_mean": round(float(kms.mean()), 4),
                 "note": "per-rank step time of the N-rank path (render of 1/N of the tiles, RCCL gather, unpack "

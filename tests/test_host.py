@@ -258,23 +258,31 @@ def test_tiles_per_rank():
     g = vd.deal_block()
     assert g >= 1
     assert vrt.tiles_per_rank(f, 8) == vd.tiles_per_rank(1920, 1080, 8)
-    if g == 4:  # 1980 whole 4x4 blocks (248 or 247 per rank) + 720 bottom-strip tiles (90 per rank)
-        assert vrt.tiles_per_rank(f, 8) == 248 * 16 + 90
+    if g == 4:  # 1980 whole 4x4 blocks (rank 0: 220, the others 251 or 252) + 720 bottom-strip tiles (90 per rank)
+        assert vrt.tiles_per_rank(f, 8) == 252 * 16 + 90
     assert vrt.tiles_per_rank(vrt.Film(1, 1, 7, 7), 1) == 0
 
 
 @pytest.mark.parametrize("nx,ny", [(1920, 1080), (3840, 2160), (200, 120), (44, 36), (64, 8), (8, 64), (256, 256)])
-@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+@pytest.mark.parametrize("nranks", [1, 2, 3, 4, 5, 8, 16])
 def test_tile_deal_matches_python_reference(nx, ny, nranks):
     """The C tile deal (vrt_internal.h tile_deal: deal_slot, with deal_tile
     checked as its inverse inside vrt_tile_deal_map) equals dist.py's
-    restatement, and the shares differ by at most one block + one tile."""
+    restatement; the shares of ranks >= 1 (all ranks below 4) differ by at
+    most one block + one tile, and from 4 ranks on rank 0 gets (m-1)/m of a
+    share (within one period's turns)."""
     f = vrt.Film(1, 1, nx, ny)
     rk, sl = vrt.tile_deal_map(f, nranks)
     prk, psl, cnt = vd.deal_owner(nx, ny, nranks)
     assert np.array_equal(rk, prk) and np.array_equal(sl, psl)
     g = vd.deal_block() if nranks > 1 else 1
-    assert cnt.max() - cnt.min() <= g * g + 1
+    m, period = vd.deal_weight(nranks)
+    rest = cnt[1:] if m else cnt
+    assert rest.max() - rest.min() <= g * g + 1
+    if m:
+        blocks = (nx // 8 // g) * (ny // 8 // g)
+        per = blocks // period  # whole periods
+        assert abs(cnt[0] - (m - 1) * per * g * g - (cnt[1] - m * per * g * g)) <= 2 * g * g + 2
     assert vrt.tiles_per_rank(f, nranks) == cnt.max()
 
 

@@ -174,8 +174,18 @@ __host__ __device__ inline void queue_range(int units, int x, int &lo, int &hi)
 // its leftover tiles.  A rank's share is so made of compact G x G regions
 // (rays of one region walk the same part of the octree), and every rank gets
 // the same number of blocks +-1.  G = 1 is tile t -> rank t % nranks.
+//
+// Rank 0 lighter (VRT_DEAL_WEIGHT, nranks >= 4): rank 0 also gathers and
+// re-assembles the frame, so it is dealt (m-1)/m of another rank's blocks,
+// m = max(2, 64 / nranks) (7/8 at 8 ranks, 15/16 at 4).  The whole blocks
+// then run in periods of V = m*nranks - 1: position pos = j % V of block j
+// goes to rank nranks-1 - pos % nranks (ranks in descending order, rank 0's
+// last turn of the period left out); a rank's blocks keep raster order.
 #ifndef VRT_DEAL_BLOCK
 #define VRT_DEAL_BLOCK 4
+#endif
+#ifndef VRT_DEAL_WEIGHT
+#define VRT_DEAL_WEIGHT 1
 #endif
 struct TileDeal {
         int ntx, nty, nranks, G;
@@ -184,6 +194,7 @@ struct TileDeal {
         int rw;      // width of the right strip (ntx - bx*G)
         int nA;      // tiles of the right strip
         int L;       // leftover tiles (right strip + bottom strip)
+        int m, V;    // weighted deal: turns per period of ranks >= 1, period (V = 0: plain round robin)
 };
 __host__ __device__ inline TileDeal tile_deal(int ntx, int nty, int nranks)
 {
@@ -198,11 +209,22 @@ __host__ __device__ inline TileDeal tile_deal(int ntx, int nty, int nranks)
         d.rw = ntx - d.bx * d.G;
         d.nA = d.by * d.G * d.rw;
         d.L = ntx * nty - d.F * d.G * d.G;
+        d.m = VRT_DEAL_WEIGHT && nranks >= 4 ? (64 / nranks > 2 ? 64 / nranks : 2) : 0;
+        d.V = d.m ? d.m * nranks - 1 : 0;
         return d;
+}
+// blocks of rank r in one period of the weighted deal
+__host__ __device__ inline int deal_turns(const TileDeal &d, int r)
+{
+        return r == 0 ? d.m - 1 : d.m;
 }
 // whole blocks of rank r, and the first leftover index it owns
 __host__ __device__ inline int deal_blocks(const TileDeal &d, int r)
 {
+        if (d.V) {
+                const int q = d.nranks - 1 - r, rem = d.F % d.V;
+                return (d.F / d.V) * deal_turns(d, r) + (rem > q ? (rem - 1 - q) / d.nranks + 1 : 0);
+        }
         return r < d.F ? (d.F - r + d.nranks - 1) / d.nranks : 0;
 }
 __host__ __device__ inline int deal_l0(const TileDeal &d, int r)
@@ -225,7 +247,12 @@ __host__ __device__ inline void deal_tile(const TileDeal &d, int r, int k, int &
         }
         const int G2 = d.G * d.G, nb = deal_blocks(d, r);
         if (k < nb * G2) {
-                const int j = r + (k / G2) * d.nranks, w = k % G2;
+                const int kb = k / G2, w = k % G2;
+                int j = r + kb * d.nranks;
+                if (d.V) {
+                        const int c = deal_turns(d, r);
+                        j = (kb / c) * d.V + (d.nranks - 1 - r) + (kb % c) * d.nranks;
+                }
                 tx = (j % d.bx) * d.G + w % d.G;
                 ty = (j / d.bx) * d.G + w / d.G;
                 return;
@@ -244,9 +271,15 @@ __host__ __device__ inline void deal_tile(const TileDeal &d, int r, int k, int &
 __host__ __device__ inline void deal_slot(const TileDeal &d, int tx, int ty, int &r, int &k)
 {
         if (tx < d.bx * d.G && ty < d.by * d.G) {
-                const int j = (ty / d.G) * d.bx + tx / d.G;
-                r = j % d.nranks;
-                k = (j / d.nranks) * d.G * d.G + (ty % d.G) * d.G + tx % d.G;
+                const int j = (ty / d.G) * d.bx + tx / d.G, w = (ty % d.G) * d.G + tx % d.G;
+                if (d.V) {
+                        const int pos = j % d.V;
+                        r = d.nranks - 1 - pos % d.nranks;
+                        k = ((j / d.V) * deal_turns(d, r) + pos / d.nranks) * d.G * d.G + w;
+                } else {
+                        r = j % d.nranks;
+                        k = (j / d.nranks) * d.G * d.G + w;
+                }
                 return;
         }
         const int li = ty < d.by * d.G ? ty * d.rw + (tx - d.bx * d.G) : d.nA + (ty - d.by * d.G) * d.ntx + tx;

@@ -11,7 +11,7 @@ The tile deal (include/vrt.h, vrt_internal.h `tile_deal`): the render area
 is the ntx x nty grid of 8x8-pixel tiles (ntx = nx//8, nty = ny//8).  With
 G = the library's deal block (G = 1 for one rank), the whole G x G blocks of
 tiles are dealt round-robin in block raster order (block j -> rank
-j % nranks); the tiles outside the whole-block region -- the right strip
+j % nranks; from 4 ranks on rank 0 gets fewer, see deal_weight); the tiles outside the whole-block region -- the right strip
 (rows above the bottom strip), then the bottom strip, each in raster order
 -- continue the deal one tile at a time (leftover i -> rank (F + i) %
 nranks, F = whole blocks).  A rank's k-th tile: its blocks' tiles first
@@ -35,6 +35,18 @@ def deal_block():
     return int(lib().vrt_tile_deal_block())
 
 
+def deal_weight(nranks):
+    """(m, V) of the weighted deal (vrt_internal.h VRT_DEAL_WEIGHT): from 4
+    ranks on, rank 0 -- which also gathers and re-assembles the frame -- gets
+    (m-1)/m of another rank's blocks, m = max(2, 64 // nranks); the whole
+    blocks run in periods of V = m*nranks - 1 turns, position p of a period
+    going to rank nranks-1 - p % nranks.  (0, 0): plain round robin."""
+    if nranks < 4:
+        return 0, 0
+    m = max(2, 64 // nranks)
+    return m, m * nranks - 1
+
+
 def deal_owner(nx, ny, nranks, g=None):
     """(nty, ntx) arrays: each tile's rank and its index k in that rank's list."""
     ntx, nty = tile_grid(nx, ny)
@@ -44,8 +56,9 @@ def deal_owner(nx, ny, nranks, g=None):
     rank = np.zeros((nty, ntx), np.int64)
     slot = np.zeros((nty, ntx), np.int64)
     counts = np.zeros(nranks, np.int64)
+    m, period = deal_weight(nranks)
     for j in range(nfull):  # whole blocks, block raster order
-        r = j % nranks
+        r = nranks - 1 - (j % period) % nranks if period else j % nranks
         y0, x0 = (j // bx) * g, (j % bx) * g
         for w in range(g * g):
             ty, tx = y0 + w // g, x0 + w % g
