@@ -16,7 +16,8 @@ HIPFLAGS := -x hip --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 $(FP) -Iinclude -
             -Wall -Wno-unused-function -fvisibility=hidden
 CXXFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Wall -fvisibility=hidden
 
-HOSTOBJS := $(BLD)/vrt_host.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o
+LIBS := -L/opt/rocm/lib -lrccl -lpthread
+HOSTOBJS := $(BLD)/vrt_host.o $(BLD)/vrt_multi.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o
 OBJS := $(BLD)/vrt_kernels.o $(BLD)/vrt_build.o $(HOSTOBJS) $(BLD)/vrt_build_id.o
 HDRS := include/vrt.h $(SRC)/vrt_math.h $(SRC)/vrt_internal.h $(SRC)/vrt_error.h
 
@@ -36,6 +37,10 @@ $(BLD)/vrt_build.o: $(SRC)/vrt_build.hip $(HDRS) | $(BLD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BLD)/vrt_host.o: $(SRC)/vrt_host.cpp $(HDRS) | $(BLD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# the multi-device frame: RCCL (ncclCommInitAll + ncclGather over xGMI)
+$(BLD)/vrt_multi.o: $(SRC)/vrt_multi.cpp $(HDRS) | $(BLD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BLD)/vrt_hdr.o: $(SRC)/vrt_hdr.cpp include/vrt.h | $(BLD)
@@ -61,7 +66,7 @@ $(BLD)/vrt_build_id.o: $(BLD)/vrt_build_id.c
 FORCE:
 
 $(PKG)/libvrt.so: $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) $(LIBS)
 
 oracle:
 	$(MAKE) -C oracle
@@ -71,16 +76,16 @@ variant: $(HOSTOBJS) $(BLD)/vrt_build.o | $(BLD)
 	mkdir -p build/variants
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
-	  build/variants/k_$(NAME).o $(BLD)/vrt_build.o $(HOSTOBJS) $(BLD)/vrt_build_id.o -lpthread
+	  build/variants/k_$(NAME).o $(BLD)/vrt_build.o $(HOSTOBJS) $(BLD)/vrt_build_id.o $(LIBS)
 
 # variant that also rebuilds the host side (for data-layout changes)
-fullvariant: $(BLD)/vrt_build.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o | $(BLD)
+fullvariant: $(BLD)/vrt_build.o $(BLD)/vrt_multi.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o | $(BLD)
 	mkdir -p build/variants
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_host.cpp -o build/variants/h_$(NAME).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
-	  build/variants/k_$(NAME).o build/variants/h_$(NAME).o $(BLD)/vrt_build.o \
-	  $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o $(BLD)/vrt_build_id.o -lpthread
+	  build/variants/k_$(NAME).o build/variants/h_$(NAME).o $(BLD)/vrt_build.o $(BLD)/vrt_multi.o \
+	  $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o $(BLD)/vrt_build_id.o $(LIBS)
 
 # ISA listing + register/occupancy report of the kernels (for DESIGN.md)
 isa: | $(BLD)

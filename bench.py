@@ -6,11 +6,12 @@ BASELINE.json configs[1]), over the 16-pose camera sweep.
 
 One process per GPU.  A step = one 1920x1080 frame (4 samples / pixel) at
 sweep pose (step % 16): each rank renders its share of the 8x8-pixel tiles
-(tile t -> rank t % N), then one RCCL gather of the per-rank tile buffers to
-rank 0, which re-assembles the image (scaling "strong": the frame is fixed).
+(the tile deal of include/vrt.h: 4x4-tile blocks round-robin, rank 0 lighter
+from 4 ranks on), then one RCCL gather of the per-rank tile buffers to rank
+0, which re-assembles the image (scaling "strong": the frame is fixed).
 Inputs (octree, triangles, textures) are resident in HBM before timing.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]   (N > 1: spawns N rank processes)
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line on stdout; diagnostics go to stderr.
@@ -286,6 +287,9 @@ def parse():
                         "tiles as one of R ranks, RCCL gather over a 1-rank process group, unpack of R rank "
                         "buffers -- the per-rank GPU and host cost of the multi-GPU step without the xGMI "
                         "transfer (reported as 'rehearsal', never as the N-GPU value)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher check only: form the process group (gloo), count the ranks, print one line; "
+                        "no GPU is used")
     a = p.parse_args()
     trace = a.mode == "trace"
     a.width = a.width or (1024 if trace else 1920)
@@ -294,13 +298,70 @@ def parse():
     return a
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE): run
+    N rank processes of this same command line (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, one GPU each), as
+    torch.distributed.run would, and exit with the worst exit code.  Called
+    before anything touches the GPU; the ranks are child processes (no exec
+    from this process)."""
+    import signal
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        for p in procs:
+            rc = max(rc, abs(p.wait()))
+            if rc:  # a failed rank: the others would wait for it in a collective
+                for q in procs:
+                    if q.poll() is None:
+                        os.killpg(q.pid, signal.SIGTERM)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                os.killpg(q.pid, signal.SIGKILL)
+    return rc
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # never fall back silently to one rank: N GPUs means N rank processes
+        sys.exit(spawn_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus={a.gpus}; using WORLD_SIZE")
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus={a.gpus}: launch one rank per GPU "
+                         f"(torch.distributed.run --nproc-per-node {a.gpus}, or bench.py --gpus {a.gpus} alone)")
+    if a.dry_run:
+        # launcher check without a GPU: the process group forms and every
+        # rank is counted (gloo on the host)
+        if world > 1:
+            dist.init_process_group("gloo")
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            seen = int(t.item())
+        else:
+            seen = 1
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": a.gpus, "ranks_seen": seen}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -312,6 +373,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev, pg_options=nccl_options())
         else:
             dist.init_process_group("gloo")
+        assert dist.get_world_size() == a.gpus, (dist.get_world_size(), a.gpus)
     elif rehearse:
         # a 1-rank RCCL group: the gather below runs through RCCL exactly as
         # in the N-rank step (its payload stays on this GPU)
@@ -577,8 +639,9 @@ def main():
         eh = (time.perf_counter() - th) / n_h
         host_out = {"ms_per_step": round(eh * 1e3, 4), "value": round(rays_per_frame / eh / 1e6, 2),
                     "unit": "Mrays/s", "frames": n_h,
-                    "note": "vrt_render into a host float RGB array (24.9 MB at 1080p over PCIe per frame), "
-                            "device buffers allocated per call"}
+                    "note": "vrt_render into a host float RGB array (24.9 MB at 1080p over PCIe per frame): "
+                            "4 tile-row bands on 2 streams, each copied D2H into pinned staging as it is "
+                            "rendered, then to the caller's array by 4 host threads"}
 
     # one launch alone: the same frames with one frame in flight (the
     # roofline's time_basis; equal to frame_ms when nfl == 1)
@@ -761,7 +824,7 @@ def main():
         value = total_rays / elapsed / 1e6
         out = {
             "metric": metric,
-            "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
+            "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "ranks_seen": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32+f64",
             "data": data_desc + ", 16-pose camera sweep",

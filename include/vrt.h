@@ -246,6 +246,10 @@ int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
  * unit to its exact fallback pass (k_render_defer), so tests can pin that
  * rarely taken path against the oracle.  0 = normal operation. */
 #define VRT_TEST_FORCE_DEFER 1
+/* VRT_TEST_FAIL_LAUNCH makes every fast-path render launch report a launch
+ * failure after its first kernel is enqueued (the error path that must
+ * leave the scene's work-queue slot usable by later launches). */
+#define VRT_TEST_FAIL_LAUNCH 2
 int vrt_set_test_flags(int flags);
 
 /* The kernels' own travorder sort (std::sort of the 8 Items by dist,
@@ -263,6 +267,42 @@ int vrt_device_selftest_order(int device, const float *dist,
                               uint32_t *orders, const float *depth,
                               const int32_t *len, int64_t m, int32_t stride,
                               int32_t *argmin);
+
+/* ---- multi-device frame (render_mt, VRT/camera.h:42-68,
+ * over the GPUs of one node) --------------------------------------------------
+ * One handle for the scene replicated on every device of `device_mask` (bit d
+ * = HIP device d; rank i = the i-th set bit, rank 0 = the lowest device, which
+ * receives and re-assembles the frame) and an RCCL communicator over them
+ * (ncclCommInitAll; RCCL is linked into libvrt.so).  The octree is built once
+ * on the host (or on the first device with VRT_BUILD_DEVICE) and uploaded to
+ * every device.  A frame: rank i renders its tiles of the tile deal
+ * (vrt_render_tiles_device with rank i of n) on its device's stream, one
+ * ncclGather of the packed tile buffers to rank 0 over xGMI (rank 0's share
+ * rendered in place into the receive buffer), then vrt_unpack_tiles_device
+ * on rank 0.  Pixels are the single-device render's, bit for bit. */
+typedef struct vrt_multi vrt_multi;
+int vrt_scene_create_multi(const vrt_scene_desc *desc, int max_depth,
+                           uint32_t device_mask, int flags, vrt_multi **out);
+void vrt_multi_destroy(vrt_multi *m);
+/* devices[i] = rank i's HIP device (n entries, n = set bits of the mask). */
+int vrt_multi_devices(const vrt_multi *m, int *n, int32_t *devices);
+/* Rank i's scene (borrowed, owned by m): info, single-device entry points. */
+int vrt_multi_scene(vrt_multi *m, int rank, vrt_scene **out);
+/* The whole frame into a host nx*ny*3 array (index y*nx+x, as vrt_render). */
+int vrt_render_multi(vrt_multi *m, const vrt_camera *cam,
+                     const vrt_film *film, float *rgb);
+/* The whole frame into d_image (nx*ny*3 floats on rank 0's device), ordered
+ * after the work already queued on `stream` (a hipStream_t of rank 0's
+ * device); work queued on `stream` afterwards sees the image.  stream = NULL:
+ * the call returns when the image is complete.  The ranks' renders and the
+ * gather run on streams owned by m. */
+int vrt_render_multi_device(vrt_multi *m, const vrt_camera *cam,
+                            const vrt_film *film, float *d_image,
+                            void *stream);
+/* The deal of a frame over the devices of a mask (host, no device): per
+ * tile ty*ntx+tx, its device and its index in that device's buffer. */
+int vrt_multi_tile_map(const vrt_film *film, uint32_t device_mask,
+                       int32_t *device_of_tile, int32_t *slot_of_tile);
 
 /* ---- full trace() (VRT/main.cc:10-30, 79-123) -------
  * The reference's actual image: a light pass from a light camera

@@ -85,3 +85,31 @@ def test_partition_covers_every_tile_and_pixel_once():
             area = np.zeros((ny, nx), int)
             area[:8 * (ny // 8), :8 * (nx // 8)] = 1
             assert np.array_equal(m, area)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_spawns_one_rank_per_gpu(n):
+    """`python bench.py --gpus N` without a launcher starts N rank processes
+    (never a silent 1-rank run): in --dry-run mode (gloo, no GPU) rank 0
+    reports N ranks seen by an all_reduce over the group."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n), "--dist-backend", "gloo",
+                        "--dry-run"], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert lines == [{"dry_run": True, "n_gpus": n, "ranks_seen": n}]
+
+
+def test_bench_refuses_world_size_mismatch():
+    """A launcher world size that differs from --gpus is an error, not a
+    silently smaller run."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--dry-run"], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode != 0 and "WORLD_SIZE=1 but --gpus=4" in p.stderr

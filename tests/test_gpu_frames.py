@@ -219,6 +219,72 @@ def test_forced_defer_pass_matches_oracle(proxy):
         assert np.array_equal(bits(got), bits(want))
 
 
+def _frame_ms(tree, cam, film, img, n):
+    """Mean device time of n production launches into img (HIP events)."""
+    import torch
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for k in range(n):
+        ev[k][0].record()
+        tree.render_tiles_device(cam, film, 0, 1, 1, img.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+
+def test_fully_deferred_frame_runs_on_the_whole_chip(proxy):
+    """A 1080p frame whose every unit is deferred (VRT_TEST_FORCE_DEFER: the
+    camera-independent way to make every wave take the exact path) is
+    re-rendered by k_render_defer on a grid as large as the persistent
+    launch's, so it is bit-exact vs the oracle and takes less than 2x the
+    normal frame (one 4-wave workgroup took ~40x)."""
+    import torch
+    tree, osc = scenes(proxy, 8)
+    mn, mx = tree.root_box
+    p = vrt.sweep_pose(mn, mx, 13, 16)
+    cam, film = vrt.Camera(*p), vrt.Film(1, 1, 1920, 1080)
+    want = osc.render(po.camera(*p), 1.0, 1.0, 1920, 1080, nthreads=NTH, samples=False)
+    img = torch.zeros((1080, 1920, 3), dtype=torch.float32, device="cuda:0")
+    _frame_ms(tree, cam, film, img, 2)
+    normal = _frame_ms(tree, cam, film, img, 8)
+    assert np.array_equal(bits(img.cpu().numpy()), bits(want))
+    try:
+        vrt.set_test_flags(vrt.TEST_FORCE_DEFER)
+        img.zero_()
+        deferred = _frame_ms(tree, cam, film, img, 8)
+        assert np.array_equal(bits(img.cpu().numpy()), bits(want))
+    finally:
+        vrt.set_test_flags(0)
+    print(f"normal {normal:.3f} ms, every unit deferred {deferred:.3f} ms")
+    assert deferred < 2.0 * normal, (normal, deferred)
+
+
+@pytest.mark.parametrize("flags", [vrt.TEST_FAIL_LAUNCH, vrt.TEST_FAIL_LAUNCH | vrt.TEST_FORCE_DEFER])
+def test_failed_launch_leaves_work_queue_usable(proxy, flags):
+    """A launch that fails after its first kernel was enqueued (test hook
+    VRT_TEST_FAIL_LAUNCH; with FORCE_DEFER its deferred list is non-empty
+    too) reports VRT_E_DEVICE, and its work-queue slot is reset on the
+    stream: the next 12 launches (every slot of the ring, the failed one
+    included) equal the oracle's image."""
+    import torch
+    tree, osc = scenes(proxy, 8)
+    mn, mx = tree.root_box
+    p = vrt.sweep_pose(mn, mx, 8, 16)
+    cam, film = vrt.Camera(*p), vrt.Film(1, 1, 320, 200)
+    want = osc.render(po.camera(*p), 1.0, 1.0, 320, 200, nthreads=NTH, samples=False)
+    img = torch.zeros((200, 320, 3), dtype=torch.float32, device="cuda:0")
+    torch.cuda.synchronize()
+    try:
+        vrt.set_test_flags(flags)
+        for _ in range(3):
+            with pytest.raises(vrt.VrtError):
+                tree.render_tiles_device(cam, film, 0, 1, 1, img.data_ptr(), None)
+    finally:
+        vrt.set_test_flags(0)
+    torch.cuda.synchronize()
+    for _ in range(12):
+        assert np.array_equal(bits(_device_image(tree, cam, film)), bits(want))
+
+
 @pytest.mark.parametrize("near,far", [(0.05, vrt.FLT_MAX), (0.0, 2.5), (-1.0, 1e30)])
 def test_general_persistent_kernel_nonstandard_range_matches_oracle(proxy, near, far):
     """A camera with near != +0 or far != FLT_MAX makes rays outside the
@@ -297,3 +363,54 @@ def test_device_build_matches_oracle(depth):
         for x, y in zip(g.leaves(), o.leaves()):
             assert np.array_equal(x, y)
         assert g.info.build_device_ms > 0
+
+
+def test_host_output_path_matches_oracle(proxy):
+    """vrt_render into a host array (the render_mt replacement a C++ caller
+    gets): tile-row bands on two streams, pinned staging, threaded copy-out.
+    Films of several shapes in a row (the kept device image is re-zeroed on a
+    shape change: pixels outside the tile grid stay 0), each equal to the
+    oracle's image; a film without a whole tile is all zero."""
+    tree, osc = scenes(proxy, 8)
+    mn, mx = tree.root_box
+    for k, (nx, ny) in enumerate([(1920, 1080), (204, 122), (64, 8), (1920, 1080), (7, 7), (333, 250)]):
+        p = vrt.sweep_pose(mn, mx, 3 + k, 16)
+        got = tree.render(vrt.Camera(*p), vrt.Film(1, 1, nx, ny))
+        want = osc.render(po.camera(*p), 1.0, 1.0, nx, ny, nthreads=NTH, samples=False)
+        assert np.array_equal(bits(got), bits(want)), (nx, ny)
+    # batched ray_march through the kept buffers: two sizes, then the first again
+    cam = vrt.Camera(*vrt.sweep_pose(mn, mx, 2, 16))
+    f = vrt.Film(1, 1, 64, 48)
+    rays = np.concatenate([cam.gen_rays4(f, px, py) for py in range(48) for px in range(0, 64, 4)])
+    for n in (len(rays), 17, len(rays)):
+        got = tree.ray_march(rays[:n])
+        want = osc.ray_march(rays[:n])
+        for key in ("hit", "tri", "voxel"):
+            assert np.array_equal(got[key], want[key]), (n, key)
+
+
+@pytest.mark.parametrize("nx,ny,depth", [(1920, 1080, 8), (3840, 2160, 9), (204, 122, 8)])
+def test_multi_device_frame_one_device_matches_oracle(proxy, nx, ny, depth):
+    """vrt_scene_create_multi / vrt_render_multi with device_mask = 1: a
+    1-device RCCL communicator (ncclCommInitAll) and the same path as N
+    devices -- share render, ncclGather to rank 0 (in place), unpack -- equal
+    to the oracle's image, through the host and the device entry points."""
+    import torch
+    m = vrt.MultiOctree(proxy, depth, device_mask=1)
+    try:
+        assert m.devices == [0]
+        osc = scenes(proxy, depth)[1]
+        mn, mx = m.root_box
+        for pose in (4, 10):
+            p = vrt.sweep_pose(mn, mx, pose, 16)
+            want = osc.render(po.camera(*p), 1.0, 1.0, nx, ny, nthreads=NTH, samples=False)
+            got = m.render(vrt.Camera(*p), vrt.Film(1, 1, nx, ny))
+            assert np.array_equal(bits(got), bits(want)), pose
+            img = torch.full((ny, nx, 3), 7.0, dtype=torch.float32, device="cuda:0")
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            m.render_device(vrt.Camera(*p), vrt.Film(1, 1, nx, ny), img.data_ptr(), s.cuda_stream)
+            s.synchronize()
+            assert np.array_equal(bits(img.cpu().numpy()), bits(want)), pose
+    finally:
+        m.close()

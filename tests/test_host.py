@@ -341,3 +341,40 @@ def test_stbi_write_hdr_is_the_reference_entry_point(tmp_path):
         assert p.read_bytes() == z[f"bytes{i}"].tobytes(), i
     assert vrt.lib().stbi_write_hdr(str(tmp_path / "no" / "x.hdr").encode(), 1, 1, 3,
                                     np.zeros(3, np.float32).ctypes.data_as(vrt._ffi.f32p)) == 0
+
+
+@pytest.mark.parametrize("mask", [0b11, 0b1010, 0b111, 0b10110001, 0b1111, 0b111110, 0b1110111, 0xFF])
+@pytest.mark.parametrize("film", [(1920, 1080), (3840, 2160), (204, 122), (64, 8)])
+def test_multi_device_deal_covers_every_tile_once(mask, film):
+    """vrt_multi_tile_map (host): the multi-device frame's deal for device
+    masks of 2-8 devices -- every tile goes to a device of the mask, device
+    d's slots are 0..count-1 with no gap or repeat, counts fit the packed
+    buffers (vrt_tiles_per_rank), rank i = the i-th set bit of the mask, and
+    it is the single-process tile deal (vrt_tile_deal_map) renamed by device."""
+    nx, ny = film
+    f = vrt.Film(1, 1, nx, ny)
+    devs = [d for d in range(32) if mask >> d & 1]
+    n = len(devs)
+    dv, sl = vrt.multi_tile_map(f, mask)
+    rk, sl0 = vrt.tile_deal_map(f, n)
+    assert np.array_equal(sl, sl0)
+    assert np.array_equal(dv, np.array(devs, np.int32)[rk])
+    tpr = vrt.tiles_per_rank(f, n)
+    counts = []
+    for d in devs:
+        s = np.sort(sl[dv == d])
+        assert np.array_equal(s, np.arange(len(s))), d
+        counts.append(len(s))
+    assert sum(counts) == (nx // 8) * (ny // 8)
+    assert max(counts) == tpr
+    assert set(np.unique(dv)) <= set(devs)
+
+
+def test_multi_device_create_rejects_bad_masks():
+    sd = vrt.SceneData(np.zeros((1, 9), np.float32), np.ones((1, 9), np.float32))
+    with pytest.raises(vrt.VrtError) as e:
+        vrt.MultiOctree(sd, 3, device_mask=0)
+    assert e.value.status == _ffi.VRT_E_INVALID
+    with pytest.raises(vrt.VrtError) as e:  # device 31 is never visible (none here)
+        vrt.MultiOctree(sd, 3, device_mask=1 << 31)
+    assert e.value.status == _ffi.VRT_E_NODEVICE

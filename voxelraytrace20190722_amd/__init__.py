@@ -7,15 +7,16 @@ the library and raises if it is missing: there is no CPU fallback.
 """
 from ._ffi import VrtError, lib, LIB_PATH  # noqa: F401
 from .api import (  # noqa: F401
-    FLT_MAX, Camera, Film, ObjModel, SceneData, VoxelOctree, build_id, device_count, device_selftest,
+    FLT_MAX, Camera, Film, MultiOctree, ObjModel, SceneData, VoxelOctree, multi_tile_map, build_id, device_count, device_selftest,
     device_selftest_order,
     hdr_bytes, hdr_bytes_from_rgbe, intersect_triangle3, load_image, make_ray, obj2voxel, ray_march, ray_march_init,
-    TEST_FORCE_DEFER, render, set_test_flags, sweep_pose, tga_decode, tile_deal_map, tiles_per_rank, to_radian, tri_box_overlap,
+    TEST_FORCE_DEFER, TEST_FAIL_LAUNCH, render, set_test_flags, sweep_pose, tga_decode, tile_deal_map, tiles_per_rank, to_radian, tri_box_overlap,
     unpack_tiles_device, write_hdr, rgbe_device, write_hdr_device,
 )
 
 __all__ = [
-    "VrtError", "lib", "LIB_PATH", "FLT_MAX", "Camera", "Film", "SceneData", "VoxelOctree",
+    "VrtError", "lib", "LIB_PATH", "FLT_MAX", "Camera", "Film", "SceneData", "VoxelOctree", "MultiOctree",
+    "multi_tile_map",
     "device_count", "device_selftest", "hdr_bytes", "intersect_triangle3", "make_ray",
     "ray_march", "ray_march_init", "render", "sweep_pose", "tile_deal_map", "tiles_per_rank", "to_radian",
     "tri_box_overlap", "unpack_tiles_device", "write_hdr", "ObjModel", "obj2voxel", "load_image",

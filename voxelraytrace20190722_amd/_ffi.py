@@ -151,6 +151,13 @@ SIGNATURES = {
     "vrt_tga_load": (C.c_int, [C.c_char_p, i32p, i32p, i32p, C.POINTER(u8p)]),
     "vrt_tga_decode": (C.c_int, [u8p, C.c_int64, i32p, i32p, i32p, C.POINTER(u8p)]),
     "vrt_image_free": (None, [u8p]),
+    "vrt_scene_create_multi": (C.c_int, [C.POINTER(SceneDesc), C.c_int, C.c_uint32, C.c_int, C.POINTER(_P)]),
+    "vrt_multi_destroy": (None, [_P]),
+    "vrt_multi_devices": (C.c_int, [_P, i32p, i32p]),
+    "vrt_multi_scene": (C.c_int, [_P, C.c_int, C.POINTER(_P)]),
+    "vrt_render_multi": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), f32p]),
+    "vrt_render_multi_device": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), _P, _P]),
+    "vrt_multi_tile_map": (C.c_int, [C.POINTER(Film), C.c_uint32, i32p, i32p]),
     "vrt_status_string": (C.c_char_p, [C.c_int]),
     "vrt_last_error": (C.c_char_p, []),
 }

@@ -452,6 +452,70 @@ class VoxelOctree:
               "vrt_render_trace_device")
 
 
+class MultiOctree:
+    """The octree replicated on every device of a mask, with an RCCL
+    communicator over them (vrt_scene_create_multi): one frame = every
+    device's share of the tile deal + one ncclGather to the first device +
+    unpack there -- render_mt (VRT/camera.h:42-68) over a node's GPUs."""
+
+    def __init__(self, scene, max_depth, device_mask=1, build_on_device=False):
+        self.scene = scene
+        h = C.c_void_p()
+        d = scene.desc()
+        flags = _ffi.VRT_BUILD_DEVICE if build_on_device else 0
+        check(lib().vrt_scene_create_multi(C.byref(d), int(max_depth), int(device_mask), flags, C.byref(h)),
+              "vrt_scene_create_multi")
+        self.h = h
+        n = C.c_int32()
+        check(lib().vrt_multi_devices(self.h, C.byref(n), None), "vrt_multi_devices")
+        devs = np.zeros(n.value, np.int32)
+        check(lib().vrt_multi_devices(self.h, C.byref(n), ptr(devs, _ffi.i32p)), "vrt_multi_devices")
+        self.devices = [int(x) for x in devs]
+        s0 = C.c_void_p()
+        check(lib().vrt_multi_scene(self.h, 0, C.byref(s0)), "vrt_multi_scene")
+        self.info = _ffi.SceneInfo()
+        check(lib().vrt_scene_info(s0, C.byref(self.info)), "vrt_scene_info")
+
+    def close(self):
+        if self.h:
+            lib().vrt_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def root_box(self):
+        return (np.array(self.info.root_min[:], np.float32), np.array(self.info.root_max[:], np.float32))
+
+    def render(self, cam, film):
+        """The whole frame -> (ny, nx, 3) float32 host image."""
+        rgb = np.zeros((film.ny, film.nx, 3), np.float32)
+        check(lib().vrt_render_multi(self.h, C.byref(cam.c), C.byref(film.c), ptr(rgb, _ffi.f32p)),
+              "vrt_render_multi")
+        return rgb
+
+    def render_device(self, cam, film, d_image_ptr, stream_ptr=None):
+        """The whole frame into a device image on the first device."""
+        check(lib().vrt_render_multi_device(self.h, C.byref(cam.c), C.byref(film.c), C.c_void_p(d_image_ptr),
+                                            C.c_void_p(stream_ptr) if stream_ptr else None),
+              "vrt_render_multi_device")
+
+
+def multi_tile_map(film, device_mask):
+    """The deal of a frame over a device mask as (nty, ntx) arrays: each
+    tile's device and its index in that device's buffer (vrt_multi_tile_map)."""
+    ntx, nty = film.nx // 8, film.ny // 8
+    dv = np.zeros((nty, ntx), np.int32)
+    sl = np.zeros((nty, ntx), np.int32)
+    check(lib().vrt_multi_tile_map(C.byref(film.c), int(device_mask), ptr(dv, _ffi.i32p), ptr(sl, _ffi.i32p)),
+          "vrt_multi_tile_map")
+    return dv, sl
+
+
 def ray_march_init(scene, max_depth, device=0):
     """gi::ray_march_init(root, voxels, max_depth) (VRT/voxel_octree.cc:67-75)."""
     return VoxelOctree(scene, max_depth, device)
@@ -593,6 +657,7 @@ def build_id():
 
 
 TEST_FORCE_DEFER = 1  # include/vrt.h VRT_TEST_FORCE_DEFER
+TEST_FAIL_LAUNCH = 2  # include/vrt.h VRT_TEST_FAIL_LAUNCH
 
 
 def set_test_flags(flags):

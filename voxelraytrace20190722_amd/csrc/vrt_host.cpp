@@ -300,6 +300,21 @@ uint32_t vox_of(uint32_t code, int depth)
 
 }  // namespace
 
+// Bands of vrt_render's host-output path: tile-row bands rendered
+// alternately on two streams (each a half-chip persistent grid, as with
+// frames in flight), each band's D2H copy queued as soon as it is rendered,
+// so the copies of the first bands run beside the renders of the last.
+constexpr int kOutBands = 4;
+struct HostOut {
+        float *d_img = nullptr;   // nx*ny*3 floats; pixels outside the tile grid stay 0
+        float *h_pin = nullptr;   // pinned staging of d_img
+        size_t bytes = 0;
+        int nx = 0, ny = 0;
+        hipStream_t st2 = nullptr, cp = nullptr;
+        hipEvent_t ev_r[kOutBands] = {}, ev_c[kOutBands] = {};
+        hipEvent_t ev_j = nullptr;  // second render stream joined back
+};
+
 struct vrt_scene {
         int device = 0;
         int max_depth = 0;
@@ -342,6 +357,14 @@ struct vrt_scene {
         // event of the last launch that used it
         hipEvent_t scratch_ev = nullptr;
         bool scratch_live = false;
+        // vrt_render's host-output path (render_to_host): a device image kept
+        // between calls, its pinned host staging copy, a second render stream
+        // and a copy stream, and an event per band
+        HostOut ho;
+        // vrt_ray_march_batch: device ray / hit buffers and pinned staging
+        // kept between calls (grown as needed)
+        void *d_rays = nullptr, *d_hits = nullptr, *h_rays = nullptr, *h_hits = nullptr;
+        int64_t rays_cap = 0;
         // every entry point that launches work on the scene holds mu (one
         // host thread at a time; device work on several streams is ordered
         // by the events above)
@@ -921,6 +944,47 @@ extern "C" int vrt_scene_create_ex(const vrt_scene_desc *d, int max_depth,
         return VRT_OK;
 }
 
+// The same scene on another device (vrt_scene_create_multi): the host-side
+// octree, leaf records and shading tables of `src` are copied, not rebuilt,
+// and uploaded to `device` exactly as vrt_scene_create uploads them.
+int vrt::scene_replicate(const vrt_scene *src, const vrt_scene_desc *d, int device, vrt_scene **out)
+{
+        *out = nullptr;
+        std::unique_ptr<vrt_scene> s(new (std::nothrow) vrt_scene);
+        if (!s)
+                return fail(VRT_E_NOMEM, "scene alloc");
+        const double t0 = now_ms();
+        try {
+                s->device = device;
+                s->max_depth = src->max_depth;
+                s->ntri = src->ntri;
+                s->nodes = src->nodes;
+                s->node_vox = src->node_vox;
+                s->refs48 = src->refs48;
+                s->refs64 = src->refs64;
+                s->wide_leaves = src->wide_leaves;
+                s->ref_tri = src->ref_tri;
+                s->tri_pos = src->tri_pos;
+                s->tri_attr = src->tri_attr;
+                s->mats = src->mats;
+                s->texs = src->texs;
+                s->tex_bytes = src->tex_bytes;
+                s->info = src->info;
+                s->level_begin = src->level_begin;
+        } catch (const std::bad_alloc &) {
+                return fail(VRT_E_NOMEM, "scene replica: out of host memory");
+        }
+        s->info.device = device;
+        s->info.build_ms = 0;
+        if (int rc = upload(s.get(), d)) {
+                vrt_scene_destroy(s.release());
+                return rc;
+        }
+        s->info.upload_ms = now_ms() - t0;
+        *out = s.release();
+        return VRT_OK;
+}
+
 extern "C" void vrt_scene_destroy(vrt_scene *s)
 {
         if (!s)
@@ -946,6 +1010,35 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                                 (void)hipEventDestroy(s->q_ev[k]);
                 if (s->scratch_ev)
                         (void)hipEventDestroy(s->scratch_ev);
+                HostOut &ho = s->ho;
+                if (ho.st2)
+                        (void)hipStreamSynchronize(ho.st2);
+                if (ho.cp)
+                        (void)hipStreamSynchronize(ho.cp);
+                if (ho.d_img)
+                        (void)hipFree(ho.d_img);
+                if (ho.h_pin)
+                        (void)hipHostFree(ho.h_pin);
+                for (int b = 0; b < kOutBands; ++b) {
+                        if (ho.ev_r[b])
+                                (void)hipEventDestroy(ho.ev_r[b]);
+                        if (ho.ev_c[b])
+                                (void)hipEventDestroy(ho.ev_c[b]);
+                }
+                if (ho.ev_j)
+                        (void)hipEventDestroy(ho.ev_j);
+                if (ho.st2)
+                        (void)hipStreamDestroy(ho.st2);
+                if (ho.cp)
+                        (void)hipStreamDestroy(ho.cp);
+                if (s->d_rays)
+                        (void)hipFree(s->d_rays);
+                if (s->d_hits)
+                        (void)hipFree(s->d_hits);
+                if (s->h_rays)
+                        (void)hipHostFree(s->h_rays);
+                if (s->h_hits)
+                        (void)hipHostFree(s->h_hits);
                 if (s->stream)
                         (void)hipStreamDestroy(s->stream);
         }
@@ -1123,15 +1216,34 @@ static int queue_release(vrt_scene *s, int slot, hipStream_t st, const int slice
         return VRT_OK;
 }
 
+// A launch failed after taking `slot`: whatever part of it was enqueued runs
+// before this memset (same stream), then the slot restarts from zero
+// counters, zero bases and an empty deferred list -- so a failed launch
+// never leaves a slot whose bases disagree with its counters (every later
+// launch on it would otherwise find its queue already drained).
+static void queue_reset(vrt_scene *s, int slot, hipStream_t st)
+{
+        (void)hipMemsetAsync(s->d_queue + (size_t)slot * kQueueWords, 0, kQueueBytes, st);
+        std::memset(s->q_base[slot], 0, sizeof s->q_base[slot]);
+        if (hipEventRecord(s->q_ev[slot], st) == hipSuccess)
+                s->q_live[slot] = true;
+}
+
 // One render launch on stream st (caller holds s->mu).
 static int render_launch(vrt_scene *s, RenderParams &p, bool instrumented, hipStream_t st)
 {
         int slot = -1;
+        (void)hipGetLastError();  // a leftover error of an earlier call is not this launch's
         if (render_kind(p, instrumented) != kRenderGrid)
                 if (int rc = queue_take(s, st, &p.q, &slot))
                         return rc;
         int waves = 0, units[8];
-        HIPCHK(launch_render(p, instrumented, st, &waves, units));
+        const hipError_t e = launch_render(p, instrumented, st, &waves, units);
+        if (e != hipSuccess) {
+                if (slot >= 0)
+                        queue_reset(s, slot, st);
+                return fail(VRT_E_DEVICE, "render launch failed: %s", hipGetErrorString(e));
+        }
         if (slot >= 0)
                 return queue_release(s, slot, st, units, waves);
         return VRT_OK;
@@ -1145,12 +1257,18 @@ static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int ra
         int slot = -1;
         WorkQueue q;
         std::memset(&q, 0, sizeof q);
+        (void)hipGetLastError();  // a leftover error of an earlier call is not this launch's
         if (secondary_uses_queue(p.sc))
                 if (int rc = queue_take(s, st, &q, &slot))
                         return rc;
         int waves = 0, units[8];
-        HIPCHK(launch_secondary(p, spp, rank, nranks, scene_res(s), d_prim, d_vis, s_hit, s_tri, s_vox,
-                                slot >= 0 ? &q : nullptr, st, &waves, units));
+        const hipError_t e = launch_secondary(p, spp, rank, nranks, scene_res(s), d_prim, d_vis, s_hit, s_tri,
+                                              s_vox, slot >= 0 ? &q : nullptr, st, &waves, units);
+        if (e != hipSuccess) {
+                if (slot >= 0)
+                        queue_reset(s, slot, st);
+                return fail(VRT_E_DEVICE, "secondary launch failed: %s", hipGetErrorString(e));
+        }
         if (slot >= 0)
                 return queue_release(s, slot, st, units, waves);
         return VRT_OK;
@@ -1249,6 +1367,132 @@ struct DevBuf {
 };
 }  // namespace
 
+// memcpy of a large host range split over up to 4 threads (pinned staging
+// <-> the caller's pageable arrays: one core's memcpy is well below PCIe)
+void vrt::par_memcpy(void *dst, const void *src, size_t bytes)
+{
+        const int nth = bytes >= ((size_t)4 << 20) ? 4 : 1;
+        if (nth == 1) {
+                std::memcpy(dst, src, bytes);
+                return;
+        }
+        auto part = [&](int j) {
+                const size_t a = (bytes * j / nth) & ~(size_t)63, b = j + 1 == nth ? bytes : (bytes * (j + 1) / nth) & ~(size_t)63;
+                std::memcpy(static_cast<char *>(dst) + a, static_cast<const char *>(src) + a, b - a);
+        };
+        std::vector<std::thread> th;
+        for (int j = 1; j < nth; ++j)
+                th.emplace_back(part, j);
+        part(0);
+        for (auto &t : th)
+                t.join();
+}
+
+// vrt_render into a host array (no per-sample outputs): the device image and
+// a pinned staging copy are kept in the scene; the frame is rendered as
+// kOutBands tile-row bands alternating over two streams (half-chip grids, so
+// a band's ramp-down runs beside the next band), each band copied D2H into
+// the pinned buffer on a copy stream as soon as it is rendered, and copied
+// on to `rgb` by up to 4 host threads as its copy lands.  The same kernels
+// and pixels as the one-launch render (a pixel's value does not depend on
+// the launch it belongs to).  Caller holds s->mu, device set.
+static int render_to_host(vrt_scene *s, const vrt_camera *cam, const vrt_film *film, float *rgb)
+{
+        HostOut &ho = s->ho;
+        const int nx = film->nx, ny = film->ny, ntx = nx / 8, nty = ny / 8;
+        const size_t bytes = (size_t)nx * ny * 12;
+        if (ntx == 0 || nty == 0) {  // no 8x8 tile: render_mt renders nothing
+                std::memset(rgb, 0, bytes);
+                return VRT_OK;
+        }
+        if (!ho.st2) {
+                HIPCHK(hipStreamCreateWithFlags(&ho.st2, hipStreamNonBlocking));
+                HIPCHK(hipStreamCreateWithFlags(&ho.cp, hipStreamNonBlocking));
+                for (int b = 0; b < kOutBands; ++b) {
+                        HIPCHK(hipEventCreateWithFlags(&ho.ev_r[b], hipEventDisableTiming));
+                        HIPCHK(hipEventCreateWithFlags(&ho.ev_c[b], hipEventDisableTiming));
+                }
+                HIPCHK(hipEventCreateWithFlags(&ho.ev_j, hipEventDisableTiming));
+        }
+        if (ho.nx != nx || ho.ny != ny) {
+                if (ho.bytes < bytes) {
+                        HIPCHK(hipStreamSynchronize(ho.cp));
+                        if (ho.d_img)
+                                (void)hipFree(ho.d_img);
+                        if (ho.h_pin)
+                                (void)hipHostFree(ho.h_pin);
+                        ho.d_img = nullptr;
+                        ho.h_pin = nullptr;
+                        ho.bytes = 0;
+                        HIPCHK(hipMalloc(&ho.d_img, bytes));
+                        HIPCHK(hipHostMalloc(&ho.h_pin, bytes, hipHostMallocDefault));
+                        ho.bytes = bytes;
+                }
+                // pixels outside the tile grid are never written: zero once per film shape
+                HIPCHK(hipMemsetAsync(ho.d_img, 0, bytes, s->stream));
+                ho.nx = nx;
+                ho.ny = ny;
+        }
+        const int nb = std::min(kOutBands, nty);
+        HIPCHK(hipEventRecord(s->ev0, s->stream));
+        HIPCHK(hipEventRecord(ho.ev_j, s->stream));
+        HIPCHK(hipStreamWaitEvent(ho.st2, ho.ev_j, 0));
+        size_t off[kOutBands + 1];
+        for (int b = 0; b < nb; ++b) {
+                const int r0 = b * nty / nb, r1 = (b + 1) * nty / nb;
+                hipStream_t st = (b & 1) ? ho.st2 : s->stream;
+                RenderParams p;
+                fill_render_params(s, cam, film, 0, 1, &p);
+                p.nty = r1 - r0;
+                p.ty0 = r0;
+                p.tiles_this_rank = ntx * (r1 - r0);
+                p.sc.grid_div = nb > 1 ? 2 : 1;
+                p.image_layout = 1;
+                p.out = ho.d_img;
+                if (int rc = render_launch(s, p, false, st))
+                        return rc;
+                HIPCHK(hipEventRecord(ho.ev_r[b], st));
+                HIPCHK(hipStreamWaitEvent(ho.cp, ho.ev_r[b], 0));
+                // band b's rows (the last band also carries the rows below the grid)
+                off[b] = b == 0 ? 0 : (size_t)8 * r0 * nx * 12;
+                off[b + 1] = b + 1 == nb ? bytes : (size_t)8 * r1 * nx * 12;
+                HIPCHK(hipMemcpyAsync(reinterpret_cast<char *>(ho.h_pin) + off[b],
+                                      reinterpret_cast<const char *>(ho.d_img) + off[b], off[b + 1] - off[b],
+                                      hipMemcpyDeviceToHost, ho.cp));
+                HIPCHK(hipEventRecord(ho.ev_c[b], ho.cp));
+        }
+        HIPCHK(hipEventRecord(ho.ev_j, ho.st2));
+        HIPCHK(hipStreamWaitEvent(s->stream, ho.ev_j, 0));
+        HIPCHK(hipEventRecord(s->ev1, s->stream));
+        s->timed = true;
+        // copy-out: band b as soon as its D2H copy has landed
+        std::atomic<bool> bad{ false };
+        const int nth = bytes >= ((size_t)4 << 20) ? 4 : 1;
+        auto work = [&](int j) {
+                for (int b = 0; b < nb; ++b) {
+                        if (hipEventSynchronize(ho.ev_c[b]) != hipSuccess) {
+                                bad = true;
+                                return;
+                        }
+                        const size_t n = off[b + 1] - off[b];
+                        const size_t a = off[b] + ((n * j / nth) & ~(size_t)63);
+                        const size_t e = j + 1 == nth ? off[b + 1] : off[b] + ((n * (j + 1) / nth) & ~(size_t)63);
+                        std::memcpy(reinterpret_cast<char *>(rgb) + a, reinterpret_cast<const char *>(ho.h_pin) + a,
+                                    e - a);
+                }
+        };
+        std::vector<std::thread> th;
+        for (int j = 1; j < nth; ++j)
+                th.emplace_back(work, j);
+        work(0);
+        for (auto &t : th)
+                t.join();
+        HIPCHK(hipStreamSynchronize(s->stream));
+        if (bad)
+                return fail(VRT_E_DEVICE, "vrt_render: device-to-host copy failed");
+        return VRT_OK;
+}
+
 extern "C" int vrt_render(vrt_scene *s, const vrt_camera *cam,
                           const vrt_film *film, float *rgb,
                           const vrt_samples *samples, vrt_stats *stats)
@@ -1261,6 +1505,10 @@ extern "C" int vrt_render(vrt_scene *s, const vrt_camera *cam,
                 return rc;
         std::lock_guard<std::mutex> lk(s->mu);
         HIPCHK(hipSetDevice(s->device));
+        const bool no_samples = !samples || !(samples->hit || samples->tri || samples->voxel || samples->rgb ||
+                                              samples->counters);
+        if (no_samples && !stats)
+                return render_to_host(s, cam, film, rgb);
         const size_t npix = (size_t)film->nx * film->ny;
         const size_t ns = npix * 4;
         const bool want_cnt = (samples && samples->counters) || stats;
@@ -1789,13 +2037,32 @@ extern "C" int vrt_ray_march_batch(vrt_scene *s, const vrt_ray *rays,
                 return VRT_OK;
         std::lock_guard<std::mutex> lk(s->mu);
         HIPCHK(hipSetDevice(s->device));
-        DevBuf dr, dh;
-        HIPCHK(hipMalloc(&dr.p, (size_t)n * sizeof(vrt_ray)));
-        HIPCHK(hipMalloc(&dh.p, (size_t)n * sizeof(vrt_hit)));
-        HIPCHK(hipMemcpy(dr.p, rays, (size_t)n * sizeof(vrt_ray), hipMemcpyHostToDevice));
-        HIPCHK(launch_ray_march(s->dev, dr.p, n, dh.p, s->stream));
+        // device buffers and pinned staging kept in the scene (grown as needed)
+        if (n > s->rays_cap) {
+                HIPCHK(hipStreamSynchronize(s->stream));
+                for (void **p : { &s->d_rays, &s->d_hits })
+                        if (*p) {
+                                (void)hipFree(*p);
+                                *p = nullptr;
+                        }
+                for (void **p : { &s->h_rays, &s->h_hits })
+                        if (*p) {
+                                (void)hipHostFree(*p);
+                                *p = nullptr;
+                        }
+                s->rays_cap = 0;
+                HIPCHK(hipMalloc(&s->d_rays, (size_t)n * sizeof(vrt_ray)));
+                HIPCHK(hipMalloc(&s->d_hits, (size_t)n * sizeof(vrt_hit)));
+                HIPCHK(hipHostMalloc(&s->h_rays, (size_t)n * sizeof(vrt_ray), hipHostMallocDefault));
+                HIPCHK(hipHostMalloc(&s->h_hits, (size_t)n * sizeof(vrt_hit), hipHostMallocDefault));
+                s->rays_cap = n;
+        }
+        par_memcpy(s->h_rays, rays, (size_t)n * sizeof(vrt_ray));
+        HIPCHK(hipMemcpyAsync(s->d_rays, s->h_rays, (size_t)n * sizeof(vrt_ray), hipMemcpyHostToDevice, s->stream));
+        HIPCHK(launch_ray_march(s->dev, s->d_rays, n, s->d_hits, s->stream));
+        HIPCHK(hipMemcpyAsync(s->h_hits, s->d_hits, (size_t)n * sizeof(vrt_hit), hipMemcpyDeviceToHost, s->stream));
         HIPCHK(hipStreamSynchronize(s->stream));
-        HIPCHK(hipMemcpy(hits, dh.p, (size_t)n * sizeof(vrt_hit), hipMemcpyDeviceToHost));
+        par_memcpy(hits, s->h_hits, (size_t)n * sizeof(vrt_hit));
         return VRT_OK;
 }
 

@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "vrt.h"
 #include "vrt_math.h"
 
 namespace vrt {
@@ -140,10 +141,15 @@ struct DevScene {
 // slot is reused only after its previous launch has finished (an event), so
 // no two launches share counters and no memset is needed.
 // After the counters: the deferred-unit list of k_render_p<true> (count in
-// defer[0], units from defer[kDeferList]); k_render_defer, launched behind
-// it on the same stream, renders them and zeroes the count.
+// defer[kDeferCount], units from defer[kDeferList]); k_render_defer,
+// launched behind it on the same stream, renders them (its waves take list
+// entries from defer[kDeferTake] and count themselves out on
+// defer[kDeferDone]) and its last wave zeroes all three words.
 constexpr int kQueueStride = 32;
 constexpr int kQueueSlots = 8;
+constexpr int kDeferCount = 0;
+constexpr int kDeferTake = 1;
+constexpr int kDeferDone = 2;
 constexpr int kDeferList = 32;
 constexpr int kDeferCap = 4096;
 constexpr size_t kQueueWords = 8 * kQueueStride + kDeferList + kDeferCap;
@@ -359,6 +365,8 @@ struct RenderParams {
         int32_t tiles_this_rank;
         int32_t image_layout;  // 1: out is nx*ny*3 image; 0: packed tiles
         int32_t test_flags;    // vrt_set_test_flags (VRT_TEST_FORCE_DEFER)
+        int32_t ty0;           // primary render: first tile row of the band rendered (the tile grid
+                               // is rows [ty0, ty0 + nty) of the film; 0 = the whole film)
         float *out;
         SampleOut so;
         WorkQueue q;           // persistent launches only
@@ -418,6 +426,12 @@ struct DeviceBuild {
 };
 hipError_t build_tree_device(int device, const float *pos, int ntri, const float root_mn[3],
                              const float root_mx[3], int max_depth, DeviceBuild *out, std::string *err);
+
+// Host helpers shared by vrt_host.cpp and vrt_multi.cpp (hidden symbols).
+// scene_replicate: src's host-side build uploaded to another device.
+int scene_replicate(const vrt_scene *src, const vrt_scene_desc *d, int device, vrt_scene **out);
+// memcpy of a large host range over up to 4 threads.
+void par_memcpy(void *dst, const void *src, size_t bytes);
 
 // Kernel launchers (vrt_kernels.hip)
 // Which primary-render kernel launch_render runs: the one-wave grid

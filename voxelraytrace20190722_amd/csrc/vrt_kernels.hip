@@ -1338,6 +1338,7 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         const CamParams &c = p.cam;
         int tx, ty;
         deal_tile(tile_deal(p.ntx, p.nty, p.nranks), p.rank, k, tx, ty);
+        ty += p.ty0;
         // pixel, sample and Camera::gen_rays4 direction (VRT/camera.cc:95-112)
         // of lane l
         auto sample_of = [&](int l, int &px, int &py, int &s, int &lx, int &ly) {
@@ -1536,8 +1537,12 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
                         if (lane == 0)
                                 atomicAdd(&g_phase[10], __builtin_amdgcn_s_memtime() - d_u0);
 #endif
-                        if (!done && lane == 0) {
-                                const uint32_t d = atomicAdd(p.q.defer, 1u);
+                        // `done` is wave-uniform (wave_fast_std is a whole-wave
+                        // vote): the append is one whole-wave take_unit, never
+                        // a lane-0-only atomic inside this loop, and every lane
+                        // stores the same word
+                        if (!done) {
+                                const uint32_t d = take_unit(p.q.defer + kDeferCount);
                                 if (d < (uint32_t)kDeferCap)
                                         p.q.defer[kDeferList + d] = (uint32_t)kq;
                         }
@@ -1545,27 +1550,40 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
         }
 }
 
-// The units k_render_p<true> deferred (normally none): one workgroup, the
-// general march (ray_march_dispatch).  More than kDeferCap deferred units:
-// every unit is rendered again here (the render is deterministic, so units
-// already written are rewritten with the same values).  The count is reset
-// for the queue slot's next launch.
-__global__ __launch_bounds__(kPersistBlock) void k_render_defer(RenderParams p)
+// The units k_render_p<true> deferred (normally none), rendered with the
+// general march (ray_march_dispatch) by a grid as large as the persistent
+// launch's, so even a frame whose every unit was deferred runs on the whole
+// chip.  No deferred unit: every wave returns after one scalar load.
+// Otherwise the waves pull list entries (more than kDeferCap deferred units:
+// every unit of the launch; the render is deterministic, so units already
+// written are rewritten with the same values) from the take counter with
+// whole-wave atomics, and the last wave to finish resets the count and both
+// counters for the queue slot's next launch (every other wave has finished
+// reading them: its done-add follows its last, returned, take).
+__global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_render_defer(RenderParams p)
 {
         __shared__ uint2 stk[kStack * kPersistBlock];
-        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-        const uint32_t n = __builtin_amdgcn_readfirstlane(p.q.defer[0]);
+        const int tid = threadIdx.x, lane = tid & 63;
+        const uint32_t n = __builtin_amdgcn_readfirstlane(p.q.defer[kDeferCount]);
+        if (n == 0u)
+                return;
         const uint32_t units = (uint32_t)p.tiles_this_rank * 4u;
         const bool all = n > (uint32_t)kDeferCap;
         const uint32_t m = all ? units : n;
-        for (uint32_t i = (uint32_t)wave; i < m; i += kPersistBlock / 64) {
+        for (;;) {
+                const uint32_t i = take_unit(p.q.defer + kDeferTake);
+                if (i >= m)
+                        break;
                 const uint32_t unit = all ? i : __builtin_amdgcn_readfirstlane(p.q.defer[kDeferList + i]);
                 render_unit<false, false, kPersistBlock, false, false>(p, (int)(unit >> 2), (int)(unit & 3), lane,
                                                                         stk + tid, nullptr, nullptr);
         }
-        __syncthreads();
-        if (tid == 0)
-                p.q.defer[0] = 0u;
+        const uint32_t fin = take_unit(p.q.defer + kDeferDone);
+        if (fin == gridDim.x * (uint32_t)(kPersistBlock / 64) - 1u) {
+                p.q.defer[kDeferCount] = 0u;
+                p.q.defer[kDeferTake] = 0u;
+                p.q.defer[kDeferDone] = 0u;
+        }
 }
 
 // ---------------------------------------------------------------------------
@@ -1855,6 +1873,8 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                 return hipSuccess;
         hipLaunchKernelGGL(rp.sc.wide_leaves ? k_primary1<true> : k_primary1<false>, dim3((unsigned)((npix + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
                            rp, prim);
+        if (hipError_t e = hipGetLastError())
+                return e;
         SecondaryParams sp;
         std::memset(&sp, 0, sizeof sp);
         sp.sc = rp.sc;
@@ -2123,7 +2143,11 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 const int g = std::min(cap, need);
                 if (kind == kRenderPersistFast) {
                         hipLaunchKernelGGL(k_render_p<true>, dim3(g), dim3(kPersistBlock), 0, st, p);
-                        hipLaunchKernelGGL(k_render_defer, dim3(1), dim3(kPersistBlock), 0, st, p);
+                        if (hipError_t e = hipGetLastError())
+                                return e;
+                        if (p.test_flags & VRT_TEST_FAIL_LAUNCH)  // test hook: fail between the two launches
+                                return hipErrorLaunchFailure;
+                        hipLaunchKernelGGL(k_render_defer, dim3(g), dim3(kPersistBlock), 0, st, p);
                 } else {
                         hipLaunchKernelGGL(k_render_p<false>, dim3(g), dim3(kPersistBlock), 0, st, p);
                 }
