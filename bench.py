@@ -50,18 +50,25 @@ def log(*a):
 # One counter group per pass (MI355X_MICROARCH.md "rocprofv3 PMC slots":
 # FETCH_SIZE and WRITE_SIZE never share a pass), no tracing combined.
 # ---------------------------------------------------------------------------
-PMC_PASSES = [
+PMC_PASSES = [  # (name, counters, optional)
     ("sq", ["SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_VMEM_RD",
-            "SQ_INSTS_LDS", "SQ_INSTS_SALU", "GRBM_GUI_ACTIVE"]),
-    ("fetch", ["FETCH_SIZE"]),
-    ("write", ["WRITE_SIZE"]),
-    ("tcc", ["TCC_HIT_sum", "TCC_MISS_sum"]),
+            "SQ_INSTS_LDS", "SQ_INSTS_SALU", "GRBM_GUI_ACTIVE"], False),
+    ("fetch", ["FETCH_SIZE"], False),
+    ("write", ["WRITE_SIZE"], False),
+    ("tcc", ["TCC_HIT_sum", "TCC_MISS_sum"], False),
+    # lane utilisation and the fp64 share of the VALU issue (fp64 add / mul /
+    # fma issue at half the fp32 rate: each takes two issue slots)
+    ("valu", ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+              "SQ_INSTS_VALU_TRANS_F64", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"], True),
 ]
+# helper kernels never counted as the measured kernel
+HELPERS = ("k_render_defer", "k_primary1", "k_unpack", "k_unit_order")
 
 
 def workload_args(a):
     out = ["--width", str(a.width), "--height", str(a.height), "--depth", str(a.depth),
-           "--detail", str(a.detail), "--poses", str(a.poses), "--mode", a.mode, "--spp", str(a.spp)]
+           "--detail", str(a.detail), "--poses", str(a.poses), "--mode", a.mode, "--spp", str(a.spp),
+           "--light-n", str(a.light_n)]
     if a.scene:
         out += ["--scene", a.scene]
     if a.rehearse_ranks > 1:
@@ -69,41 +76,67 @@ def workload_args(a):
     return out
 
 
-def pmc_means(out_dir, kernel_prefix, steps):
-    """Per-dispatch means of every counter in the rocprofv3
-    *counter_collection.csv files under out_dir, over the last `steps`
-    dispatches of the kernel whose name contains kernel_prefix (the timed
-    ones; helper kernels excluded) -> (means, dispatch info) or (None, None)."""
+def short_name(kn):
+    """'void vrt::k_render_p<true>(vrt::RenderParams)' -> 'k_render_p<true>'"""
+    kn = kn.split("(")[0]
+    return kn.split("::")[-1] if "vrt::" in kn else kn
+
+
+def pmc_per_kernel(out_dir, steps):
+    """Per-frame counter totals per kernel (short name) over every dispatch
+    in the rocprofv3 *counter_collection.csv files under out_dir (the child
+    runs warm-up 0, so every dispatch belongs to one of the `steps` frames),
+    plus dispatch counts and launch geometry."""
     import csv
     rows = []
     for root, _, files in os.walk(out_dir):
         for f in files:
             if f.endswith("counter_collection.csv"):
                 rows += list(csv.DictReader(open(os.path.join(root, f))))
-    per_disp, meta = {}, {}
+    tot, disp, meta = {}, {}, {}
     for r in rows:
-        kn = r["Kernel_Name"]
-        if kernel_prefix not in kn or any(x in kn for x in ("k_render_defer", "k_primary1", "k_unpack")):
-            continue
-        d = per_disp.setdefault(int(r["Dispatch_Id"]), {})
-        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-        meta = {"kernel": kn, "grid": int(r["Grid_Size"]), "wg": int(r["Workgroup_Size"]),
-                "lds": int(r["LDS_Block_Size"]), "vgpr": int(r["VGPR_Count"]),
-                "sgpr": int(r["SGPR_Count"]), "scratch": int(r["Scratch_Size"])}
-    ids = sorted(per_disp)[-steps:]
-    if len(ids) < steps:
+        kn = short_name(r["Kernel_Name"])
+        t = tot.setdefault(kn, {})
+        t[r["Counter_Name"]] = t.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        disp.setdefault(kn, set()).add(int(r["Dispatch_Id"]))
+        meta[kn] = {"kernel": r["Kernel_Name"], "grid": int(r["Grid_Size"]), "wg": int(r["Workgroup_Size"]),
+                    "lds": int(r["LDS_Block_Size"]), "vgpr": int(r["VGPR_Count"]),
+                    "sgpr": int(r["SGPR_Count"]), "scratch": int(r["Scratch_Size"])}
+    return ({k: {c: v / steps for c, v in t.items()} for k, t in tot.items()},
+            {k: len(v) / steps for k, v in disp.items()}, meta)
+
+
+def pmc_means(out_dir, kernel_prefix, steps):
+    """Per-dispatch means of the counters of the one kernel whose short name
+    starts with kernel_prefix (helpers excluded) -> (means, dispatch info)
+    or (None, None)."""
+    per, nd, meta = pmc_per_kernel(out_dir, steps)
+    ks = [k for k in per if k.startswith(kernel_prefix) and not k.startswith(HELPERS)]
+    if len(ks) != 1 or abs(nd[ks[0]] - 1.0) > 1e-9:
         return None, None
-    names = sorted({c for i in ids for c in per_disp[i]})
-    return {c: float(np.mean([per_disp[i].get(c, 0.0) for i in ids])) for c in names}, meta
+    return per[ks[0]], meta[ks[0]]
 
 
-def run_pmc(a, kernel_prefix, save_dir=""):
+def kernel_stats(out_dir):
+    """rocprofv3 --kernel-trace --stats summary -> {short name: (calls, avg ms, total ms)}."""
+    import csv
+    out = {}
+    for root, _, files in os.walk(out_dir):
+        for f in files:
+            if f.endswith("kernel_stats.csv"):
+                for r in csv.DictReader(open(os.path.join(root, f))):
+                    out[short_name(r["Name"])] = (int(r["Calls"]), float(r["AverageNs"]) / 1e6,
+                                                  float(r["TotalDurationNs"]) / 1e6)
+    return out
+
+
+def run_pmc(a, save_dir=""):
     """Run the timed region of this workload (warm-up 0, the same `steps`
-    frames, so the same pose mix) once per counter group under rocprofv3
-    --pmc, in a child process; return per-dispatch means of every counter
-    over the kernel's last `steps` dispatches (the timed ones) plus the
-    child's own kernel time.  None if rocprofv3 is unavailable or a pass
-    fails (the bench line then says so)."""
+    frames, so the same pose mix, one frame in flight) once per counter group
+    under rocprofv3 --pmc, plus one --kernel-trace --stats pass, each in a
+    child process (tracing never combined with counters).  Returns the
+    per-frame counters per kernel, the kernel-trace summary and each pass's
+    own kernel time, or None and the reason when a required pass fails."""
     import shutil
     import signal
     import subprocess
@@ -115,12 +148,14 @@ def run_pmc(a, kernel_prefix, save_dir=""):
     env = dict(os.environ, TMPDIR="/tmp")
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    means, child_ms, meta = {}, {}, {}
-    for name, counters in PMC_PASSES:
+    child = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-counters", "--no-pmc", "--no-d9",
+             "--frames-in-flight", "1", "--warmup", "0", "--steps", str(a.steps), *workload_args(a)]
+    per, nd, meta, child_ms, skipped = {}, {}, {}, {}, []
+    stats = None
+    passes = [(n, ["--pmc", *c], opt) for n, c, opt in PMC_PASSES] + [("ktrace", ["--kernel-trace", "--stats"], False)]
+    for name, popt, optional in passes:
         out_dir = os.path.join(tmp, name)
-        cmd = [prof, "--pmc", *counters, "--output-format", "csv", "-d", out_dir, "-o", name, "--",
-               sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-counters", "--no-pmc",
-               "--no-d9", "--frames-in-flight", "1", "--warmup", "0", "--steps", str(a.steps), *workload_args(a)]
+        cmd = [prof, *popt, "--output-format", "csv", "-d", out_dir, "-o", name, "--", *child]
         t0 = time.time()
         p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                              start_new_session=True, text=True)
@@ -129,82 +164,111 @@ def run_pmc(a, kernel_prefix, save_dir=""):
         except subprocess.TimeoutExpired:
             os.killpg(p.pid, signal.SIGKILL)
             p.communicate()
+            if optional:
+                skipped.append(f"{name}: timed out")
+                continue
             return None, f"pmc pass {name} timed out"
         if p.returncode != 0:
-            return None, f"pmc pass {name} rc={p.returncode}: {se.strip().splitlines()[-1:] if se else ''}"
+            why = f"pmc pass {name} rc={p.returncode}: {se.strip().splitlines()[-1:] if se else ''}"
+            if optional:
+                skipped.append(why)
+                continue
+            return None, why
         line = [ln for ln in so.splitlines() if ln.startswith("{")]
         if line:
-            child_ms[name] = json.loads(line[-1]).get("kernel_ms_mean")
-        got, meta_ = pmc_means(out_dir, kernel_prefix, a.steps)
-        if got is None:
-            return None, f"pmc pass {name}: fewer than {a.steps} dispatches of {kernel_prefix}"
-        means.update(got)
-        meta = meta_
-        log(f"[pmc] pass {name}: {a.steps} dispatches, {time.time() - t0:.1f} s")
+            j = json.loads(line[-1])
+            child_ms[name] = j.get("trace_kernel_ms_mean", j.get("kernel_ms_mean"))
+        if name == "ktrace":
+            stats = kernel_stats(out_dir)
+        else:
+            got, n_, m_ = pmc_per_kernel(out_dir, a.steps)
+            for k, v in got.items():
+                per.setdefault(k, {}).update(v)
+            nd.update(n_)
+            meta.update(m_)
+        log(f"[pmc] pass {name}: {time.time() - t0:.1f} s")
         if save_dir:
             os.makedirs(save_dir, exist_ok=True)
             for root, _, files in os.walk(out_dir):
                 for f in files:
-                    if f.endswith(".csv"):
+                    if f.endswith(".csv") and "agent_info" not in f:
                         shutil.copy(os.path.join(root, f), os.path.join(save_dir, f"{name}_{f}"))
     shutil.rmtree(tmp, ignore_errors=True)
     # the clock comes from GRBM_GUI_ACTIVE of the "sq" pass over that pass's
     # own kernel time (profiled passes run at their own clock)
-    return {"means": means, "child_kernel_ms": child_ms.get("sq"), "dispatch": meta}, None
+    return {"per_kernel": per, "per_frame_dispatches": nd, "dispatch": meta, "child_kernel_ms": child_ms.get("sq"),
+            "kernel_stats": stats, "skipped": skipped}, None
 
 
-def roofline_from_pmc(pmc, kernel_ms, out_bytes, ref_bytes, single_ms=None):
-    """The measured roofline of the dominant kernel: VALU issue (the limiter,
-    DESIGN.md §4) -- the VALU wave-instructions of one launch (SQ_INSTS_VALU)
-    over this run's per-frame device time (frame_ms), against the issue peak at the max
-    engine clock -- and HBM traffic (FETCH_SIZE x2 per MI355X_MICROARCH.md
-    §HBM + WRITE_SIZE; rocprofv3 reports KiB) over the same time as a
-    fraction of the 8 TB/s peak.  issue_frac_at_clock is the same
-    instruction count over the issue slots of the cycles the profiled
-    launch actually ran (GRBM_GUI_ACTIVE / 8), i.e. at the measured clock."""
-    m = pmc["means"]
-    t = kernel_ms * 1e-3
+def roofline_from_pmc(pmc, kernel, single_ms, out_bytes, ref_bytes, launch_ms=None, child_ms=None):
+    """The measured roofline of one kernel (short name): VALU issue (the
+    limiter) -- its VALU wave-instructions per frame
+    (SQ_INSTS_VALU) over its time per frame alone on the GPU (single_ms: one
+    frame in flight, HIP events in this process; rocprofv3's kernel-trace
+    average of the same command is reported next to it), against the issue
+    peak at the max engine clock -- and HBM traffic (FETCH_SIZE x2 per
+    MI355X_MICROARCH.md §HBM + WRITE_SIZE; rocprofv3 reports KiB) over the
+    same time as a fraction of the 8 TB/s peak.  Also: the fp64-weighted
+    issue fraction (fp64 VALU ops take two issue slots), the lane
+    utilisation of the VALU instructions, the issue fraction at the measured
+    clock, and (launch_ms) the same with frames in flight."""
+    m = pmc["per_kernel"][kernel]
+    t = single_ms * 1e-3
     rd = 2 * m["FETCH_SIZE"] * 1024
     wr = m["WRITE_SIZE"] * 1024
     traffic = rd + wr
     cycles = m["GRBM_GUI_ACTIVE"] / 8                          # summed over the 8 XCDs
-    cms = pmc["child_kernel_ms"] or kernel_ms
+    cms = child_ms or pmc.get("child_kernel_ms") or single_ms
     clock = cycles / (cms * 1e-3) / 1e9                        # GHz in the profiled pass
-    achieved = m["SQ_INSTS_VALU"] / t / 1e9                    # G wave-instr/s
+    valu = m["SQ_INSTS_VALU"]
+    achieved = valu / t / 1e9                                  # G wave-instr/s
     peak = VALU_WAVE_INSTR_PER_CYCLE * MAX_CLOCK_GHZ           # G wave-instr/s
     hbm = traffic / t / 1e9
     h, mi = m.get("TCC_HIT_sum", 0.0), m.get("TCC_MISS_sum", 0.0)
-    return {
+    f64 = [m.get(c) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                              "SQ_INSTS_VALU_TRANS_F64")]
+    out = {
         "bound": "valu",
         "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "G wave-instr/s",
         "frac": round(achieved / peak, 4),
         "peak_def": f"{N_CU} CUs x 4 SIMDs x 1/2 wave64 VALU instr/cycle x {MAX_CLOCK_GHZ} GHz max clock",
-        "issue_frac_at_clock": round(m["SQ_INSTS_VALU"] / (VALU_WAVE_INSTR_PER_CYCLE * cycles), 4),
+        "time_basis": {"single_launch_ms": round(single_ms, 4),
+                       "note": "one frame in flight: the kernel alone on the GPU (HIP events on its stream)"},
+        "issue_frac_at_clock": round(valu / (VALU_WAVE_INSTR_PER_CYCLE * cycles), 4),
         "clock_ghz_profiled": round(clock, 3),
-        "valu_instr_per_launch": round(m["SQ_INSTS_VALU"]),
+        "valu_instr_per_launch": round(valu),
         "traffic": round(traffic),
         "hbm": {"achieved": round(hbm, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(hbm / PEAK_HBM_GBS, 4),
                 "read_bytes": round(rd), "read_bytes_raw": round(rd / 2), "write_bytes": round(wr)},
         "traffic_over_output": round(traffic / out_bytes, 2),
         "l2_hit": round(h / (h + mi), 4) if h + mi > 0 else None,
-        "valu_instr_per_wave": round(m["SQ_INSTS_VALU"] / max(1.0, m["SQ_WAVES"]), 1),
+        "valu_instr_per_wave": round(valu / max(1.0, m["SQ_WAVES"]), 1),
         "avg_waves_per_cu": round(4 * m["SQ_WAVE_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8) / N_CU, 2),
         "reference_equivalent_bytes_per_launch": ref_bytes,
-        # which launch time `achieved` divides by: with frames in flight
-        # launches overlap (the HIP-event span of one launch and rocprofv3's
-        # kernel duration then cover 2-3 frames), so the per-launch time is
-        # the step time; single_launch_ms is one launch alone (the same
-        # frames, one in flight, HIP events in this process: what the
-        # one-frame rocprofv3 kernel trace shows)
-        "time_basis": {"launch_ms": round(kernel_ms, 4), "single_launch_ms": round(single_ms or kernel_ms, 4),
-                       "achieved_single_launch": round(m["SQ_INSTS_VALU"] / ((single_ms or kernel_ms) * 1e-3) / 1e9,
-                                                       1),
-                       "frac_single_launch": round(m["SQ_INSTS_VALU"] / ((single_ms or kernel_ms) * 1e-3) / 1e9
-                                                   / peak, 4)},
-        "kernel": pmc["dispatch"].get("kernel"),
-        "dispatch": pmc["dispatch"],
+        "kernel": pmc["dispatch"].get(kernel, {}).get("kernel"),
+        "dispatch": pmc["dispatch"].get(kernel),
         "source": "live rocprofv3 --pmc passes of this bench command (counters per timed dispatch)",
     }
+    if all(v is not None for v in f64):
+        n64 = sum(f64)
+        out["fp64_instr_per_launch"] = round(n64)
+        out["frac_fp64_weighted"] = round((valu + n64) / t / 1e9 / peak, 4)
+    if m.get("SQ_THREAD_CYCLES_VALU") and m.get("SQ_ACTIVE_INST_VALU"):
+        lu = m["SQ_THREAD_CYCLES_VALU"] / (64.0 * m["SQ_ACTIVE_INST_VALU"])
+        out["lane_utilisation"] = round(lu, 4)
+        out["lane_util_def"] = "SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)"
+        out["frac_active_lanes"] = round(achieved / peak * lu, 4)
+    ks = pmc.get("kernel_stats") or {}
+    if kernel in ks:
+        calls, avg, _ = ks[kernel]
+        out["time_basis"]["rocprof_kernel_trace_avg_ms"] = round(avg, 4)
+        out["time_basis"]["rocprof_calls"] = calls
+    if launch_ms is not None and launch_ms != single_ms:
+        out["time_basis"]["launch_ms"] = round(launch_ms, 4)
+        out["time_basis"]["frac_at_launch_ms"] = round(valu / (launch_ms * 1e-3) / 1e9 / peak, 4)
+    if pmc.get("skipped"):
+        out["pmc_skipped"] = pmc["skipped"]
+    return out
 
 
 def cpu_info():
@@ -230,6 +294,14 @@ def cpu_info():
     except Exception:
         pass
     return {"nproc": n, "affinity": aff, "cgroup_quota_cpus": quota, "model": model}
+
+
+def eff_cores(nth, ci):
+    """CPUs the CPU baseline can actually use: its threads, capped by the
+    affinity mask and the job's cgroup CPU quota (16 on the GPU box, whose
+    nproc is 256)."""
+    q = ci["cgroup_quota_cpus"]
+    return int(min(nth, ci["affinity"], q if q else nth))
 
 
 def nccl_options():
@@ -632,14 +704,15 @@ def main():
     host_out = None
     if world == 1 and not rehearse and not secondary and not trace and not a.no_d9:
         n_h = min(a.steps, 16)
-        tree.render(cams[0], film)  # warm-up
+        hrgb = np.zeros((a.height, a.width, 3), np.float32)  # the caller's film, reused every frame
+        tree.render(cams[0], film, out=hrgb)  # warm-up (first touch of the film's pages)
         th = time.perf_counter()
         for k in range(n_h):
-            tree.render(cams[k % a.poses], film)
+            tree.render(cams[k % a.poses], film, out=hrgb)
         eh = (time.perf_counter() - th) / n_h
         host_out = {"ms_per_step": round(eh * 1e3, 4), "value": round(rays_per_frame / eh / 1e6, 2),
                     "unit": "Mrays/s", "frames": n_h,
-                    "note": "vrt_render into a host float RGB array (24.9 MB at 1080p over PCIe per frame): "
+                    "note": "vrt_render into the caller's host float RGB film, reused every frame (24.9 MB at 1080p over PCIe per frame): "
                             "4 tile-row bands on 2 streams, each copied D2H into pinned staging as it is "
                             "rendered, then to the caller's array by 4 host threads"}
 
@@ -689,15 +762,43 @@ def main():
         nr = cnt_tot / (len(poses_used) * rays_per_frame / world)
         per_ray = {"A": round(float(nr[0]), 2), "L": round(float(nr[1]), 2),
                    "T": round(float(nr[2]), 2), "H": round(float(nr[3]), 3)}
-    if rank == 0 and world == 1 and not trace and not a.no_pmc:
-        pmc, why = run_pmc(a, "k_secondary" if secondary else "k_render", a.pmc_save)
+    trace_kernels = None
+    if rank == 0 and world == 1 and not a.no_pmc:
+        pmc, why = run_pmc(a, a.pmc_save)
         out_bytes = (W8 * H8 * 4) if secondary else (W8 * H8 * 12 // nshare)
         if pmc:
-            roof = roofline_from_pmc(pmc, frame_ms, out_bytes, ref_bytes, single_ms)
-            if per_ray:
-                roof["per_ray"] = per_ray
-            roof["build_id"] = vrt.build_id()
-        else:
+            pk = pmc["per_kernel"]
+            ks = pmc.get("kernel_stats") or {}
+            cand = [k for k in pk if not k.startswith(HELPERS) and "SQ_INSTS_VALU" in pk[k] and "FETCH_SIZE" in pk[k]
+                    and "vrt::" in pmc["dispatch"].get(k, {}).get("kernel", "")]
+            if trace:
+                # the full frame's kernels, each against its own rocprof time;
+                # the line's roofline = the one with the most time per frame
+                trace_kernels = {}
+                for k in cand:
+                    if k in ks:
+                        calls, avg, tot = ks[k]
+                        r_ = roofline_from_pmc(pmc, k, tot / a.steps, out_bytes, None, child_ms=tot / a.steps)
+                        r_["time_basis"] = {"rocprof_ms_per_frame": round(tot / a.steps, 4),
+                                            "dispatches_per_frame": round(calls / a.steps, 2),
+                                            "note": "rocprofv3 kernel trace of this command (one frame in flight)"}
+                        trace_kernels[k] = r_
+                dom = max(trace_kernels, key=lambda k: trace_kernels[k]["time_basis"]["rocprof_ms_per_frame"]) \
+                    if trace_kernels else None
+                roof = dict(trace_kernels[dom]) if dom else None
+                if roof:
+                    roof["traffic_over_output"] = None  # the frame writes only the 1024^2 image
+            else:
+                dom = max(cand, key=lambda k: pk[k]["SQ_INSTS_VALU"]) if cand else None
+                roof = roofline_from_pmc(pmc, dom, single_ms, out_bytes, ref_bytes,
+                                         launch_ms=frame_ms) if dom else None
+            if roof is None:
+                why = f"no measured kernel among {sorted(pk)}"
+            else:
+                if per_ray:
+                    roof["per_ray"] = per_ray
+                roof["build_id"] = vrt.build_id()
+        if not pmc or roof is None:
             log(f"[pmc] no roofline: {why}")
             roof = {"bound": "valu", "achieved": None, "peak": None, "unit": "G wave-instr/s", "frac": None,
                     "traffic": None, "unavailable": why, "reference_equivalent_bytes_per_launch": ref_bytes}
@@ -724,11 +825,58 @@ def main():
                          1.0, 1.0, hw, hh, res, nthreads=nth, samples=False)
         t2_ = time.perf_counter()
         tr = (t2_ - t1_) * (a.width * a.height) / (hw * hh)
-        cpu = {"value": round(1.0 / ((t1_ - t0_) + tr), 5), "unit": "frames/s", "cores": nth, "kind": "port",
+        cpu = {"value": round(1.0 / ((t1_ - t0_) + tr), 5), "unit": "frames/s", "cores": eff_cores(nth, ci), "threads": nth, "kind": "port",
                "nproc": ci["nproc"], "cgroup_quota_cpus": ci["cgroup_quota_cpus"], "cpu_model": ci["model"],
                "sample": f"light map {a.light_n}^2 x4 + filter ({t1_ - t0_:.1f} s) + cone-traced {hw}x{hh} x4 "
                          f"({t2_ - t1_:.1f} s, scaled x{(a.width * a.height) / (hw * hh):.0f} to "
                          f"{a.width}x{a.height}) by oracle/vrt_oracle.c over {nth} threads"}
+        osc.close()
+    if rank == 0 and world == 1 and not a.no_cpu and secondary:
+        # config 5 on the oracle: render_secondary (primary hit + spp rays
+        # per pixel, VRT/voxel_octree.cc:600-603 pattern) over min(nproc, 64)
+        # threads, 1 warm-up + >= cpu_frames whole frames of the sweep; value
+        # = rays traced / the median frame time; each frame's visibility
+        # image checked bit for bit against the GPU's of the same pose
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as po
+        ci = cpu_info()
+        osc = po.Scene(sd, a.depth)
+        nth = max(1, min(a.cpu_threads or ci["nproc"], 64))
+
+        def oframe(pi):
+            fov, eye, spot, up = vrt.sweep_pose(mn, mx, pi, a.poses)
+            t0_ = time.perf_counter()
+            vis, nr = osc.render_secondary(po.camera(fov, eye, spot, up), 1.0, 1.0, a.width, a.height, spp=a.spp,
+                                           nthreads=nth, ids=False)
+            return time.perf_counter() - t0_, vis, nr
+
+        warm_s, _, _ = oframe(0)
+        times, rates, frames = [], [], 0
+        gvis = torch.zeros((a.height, a.width), dtype=torch.float32, device=dev)
+        gprim = torch.zeros(W8 * H8 * 8, dtype=torch.float32, device=dev)
+        while frames < max(5, a.cpu_frames):
+            pi = frames % a.poses
+            s_, ovis, nr = oframe(pi)
+            times.append(s_)
+            rates.append(nr / s_)
+            gvis.zero_()
+            tree.render_secondary_device(cams[pi], film, a.spp, 0, 1, gprim.data_ptr(), gvis.data_ptr(), sp)
+            torch.cuda.synchronize()
+            if not np.array_equal(gvis.cpu().numpy().view(np.uint32), ovis.view(np.uint32)):
+                raise SystemExit(f"GPU visibility image of pose {pi} differs from the CPU oracle frame")
+            if nr != frame_rays.get(pi, nr):
+                raise SystemExit(f"pose {pi}: oracle traced {nr} rays, the GPU count is {frame_rays[pi]}")
+            frames += 1
+        med = float(np.median(times))
+        cpu = {"value": round(float(np.median(rates)) / 1e6, 4), "unit": "Mrays/s", "cores": eff_cores(nth, ci), "threads": nth, "kind": "port",
+               "nproc": ci["nproc"], "affinity_cpus": ci["affinity"], "cgroup_quota_cpus": ci["cgroup_quota_cpus"],
+               "cpu_model": ci["model"],
+               "frame_s": {"warmup": round(warm_s, 3), "median": round(med, 3), "min": round(min(times), 3),
+                           "max": round(max(times), 3)},
+               "sample": f"1 warm-up + {frames} full {a.width}x{a.height} frames x (1 primary + {a.spp} secondary "
+                         f"rays per hit pixel) (sweep poses 0..{frames - 1}, median rate), oracle/vrt_oracle.c "
+                         f"render_secondary over {nth} threads; all {frames} visibility images bit-identical to "
+                         f"the GPU's of the same pose"}
         osc.close()
     if rank == 0 and world == 1 and not rehearse and not a.no_cpu and not secondary and not trace:
         # The reference's scheduler: thread_pool_cpp with hardware_concurrency
@@ -763,7 +911,7 @@ def main():
             checked += 1
             frames += 1
         med = float(np.median(times))
-        cpu = {"value": round(rays_per_frame / med / 1e6, 4), "unit": "Mrays/s", "cores": nth, "kind": "port",
+        cpu = {"value": round(rays_per_frame / med / 1e6, 4), "unit": "Mrays/s", "cores": eff_cores(nth, ci), "threads": nth, "kind": "port",
                "nproc": ci["nproc"], "affinity_cpus": ci["affinity"], "cgroup_quota_cpus": ci["cgroup_quota_cpus"],
                "cpu_model": ci["model"],
                "frame_s": {"warmup": round(warm_s, 3), "median": round(med, 3), "min": round(min(times), 3),
@@ -798,7 +946,8 @@ def main():
                            "parallelism": f"replicated light map, screen tiles x{world}"},
                 "light_ms_mean": round(float(np.mean(light_ms)), 3),
                 "trace_kernel_ms_mean": round(float(kms.mean()), 3),
-                "roofline": None,
+                "roofline": roof,
+                "roofline_per_kernel": trace_kernels,
                 "cpu_baseline": cpu,
             }
             print(json.dumps(out), flush=True)

@@ -338,10 +338,16 @@ class VoxelOctree:
                 "voxel": out[:, 2].copy(), "hit_p": out[:, 3:6].view(np.float32).copy(),
                 "normal": out[:, 6:9].view(np.float32).copy()}
 
-    def render(self, cam, film, samples=False, counters=False):
-        """Primary render -> (ny, nx, 3) float32 image (+ per-sample dict)."""
+    def render(self, cam, film, samples=False, counters=False, out=None):
+        """Primary render -> (ny, nx, 3) float32 image (+ per-sample dict).
+        out: a C-contiguous (ny, nx, 3) float32 array to render into (a film
+        reused across frames, as the reference's Film is)."""
         nx, ny = film.nx, film.ny
-        rgb = np.zeros((ny, nx, 3), np.float32)
+        if out is not None:
+            assert out.shape == (ny, nx, 3) and out.dtype == np.float32 and out.flags.c_contiguous
+            rgb = out
+        else:
+            rgb = np.zeros((ny, nx, 3), np.float32)
         smp = None
         st = None
         so = None

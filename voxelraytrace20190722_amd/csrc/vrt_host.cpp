@@ -1234,9 +1234,10 @@ static int render_launch(vrt_scene *s, RenderParams &p, bool instrumented, hipSt
 {
         int slot = -1;
         (void)hipGetLastError();  // a leftover error of an earlier call is not this launch's
-        if (render_kind(p, instrumented) != kRenderGrid)
+        if (render_kind(p, instrumented) != kRenderGrid) {
                 if (int rc = queue_take(s, st, &p.q, &slot))
                         return rc;
+        }
         int waves = 0, units[8];
         const hipError_t e = launch_render(p, instrumented, st, &waves, units);
         if (e != hipSuccess) {
@@ -1784,7 +1785,8 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         const size_t b4 = align_up((size_t)ns * 4), b24 = align_up((size_t)ns * 48);
         const int64_t max_seg = std::max<int64_t>(1, s->info.nonempty_leaves);
         const size_t bseg = align_up((size_t)max_seg * 4);
-        const size_t need = 4 * b4 + b24 + align_up(sort_bytes) + 256 + bseg;
+        const size_t bend = align_up((size_t)nnodes * 4);
+        const size_t need = 4 * b4 + b24 + align_up(sort_bytes) + 256 + bseg + bend;
         HIPCHK(ensure_light_scratch(s, need));
         char *base = static_cast<char *>(s->d_light);
         uint32_t *k_in = reinterpret_cast<uint32_t *>(base);
@@ -1797,6 +1799,7 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         unsigned long long *d_hits = reinterpret_cast<unsigned long long *>(tail);
         unsigned int *d_nseg = reinterpret_cast<unsigned int *>(tail + 64);
         uint32_t *d_seg = reinterpret_cast<uint32_t *>(tail + 256);
+        uint32_t *d_seg_end = reinterpret_cast<uint32_t *>(tail + 256 + bseg);
         HIPCHK(hipMemsetAsync(tail, 0, 256, s->stream));
         LightParams lp;
         std::memset(&lp, 0, sizeof lp);
@@ -1811,7 +1814,8 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         HIPCHK(launch_light(lp, s->stream));
         HIPCHK(launch_iota(v_in, ns, s->stream));
         HIPCHK(sort_pairs_u32(temp, &sort_bytes, k_in, k_out, v_in, v_out, ns, bits, s->stream));
-        HIPCHK(launch_lm_accum(ns, k_out, v_out, samp, miss_key, d_seg, d_nseg, max_seg, s->d_lm, s->stream));
+        HIPCHK(launch_lm_accum(ns, k_out, v_out, samp, miss_key, d_seg, d_nseg, max_seg, d_seg_end, s->d_lm,
+                               s->stream));
         // cone_trace_init_filter: leaves, then internal levels bottom-up
         HIPCHK(launch_lm_leaves(s->dev.nodes, nnodes, s->d_lm, s->stream));
         const int nlev = (int)s->level_begin.size() - 1;
@@ -1885,7 +1889,7 @@ static int trace_scratch(vrt_scene *s, const TraceParams &tp, TraceParams *out, 
         if (trace_fused())
                 return VRT_OK;
         const size_t nslots = (size_t)tp.r.tiles_this_rank * 256;
-        const size_t need = nslots * 64 + nslots * 72 + 512;  // records + 6 cone results
+        const size_t need = nslots * 64 + 512;  // the primary pass's 64-B records
         if (s->trace_bytes < need) {
                 if (s->d_trace) {
                         HIPCHK(hipDeviceSynchronize());  // callers may have queued work on any stream
@@ -1899,7 +1903,6 @@ static int trace_scratch(vrt_scene *s, const TraceParams &tp, TraceParams *out, 
         (void)st;
         char *base = static_cast<char *>(s->d_trace);
         out->rec = reinterpret_cast<float4 *>(base);
-        out->col = reinterpret_cast<float *>(base + ((nslots * 64 + 255) & ~(size_t)255));
         return VRT_OK;
 }
 

@@ -140,19 +140,24 @@ struct DevScene {
 // queue_release).  Launches on different streams use different slots; a
 // slot is reused only after its previous launch has finished (an event), so
 // no two launches share counters and no memset is needed.
-// After the counters: the deferred-unit list of k_render_p<true> (count in
-// defer[kDeferCount], units from defer[kDeferList]); k_render_defer,
-// launched behind it on the same stream, renders them (its waves take list
-// entries from defer[kDeferTake] and count themselves out on
-// defer[kDeferDone]) and its last wave zeroes all three words.
+// After the counters: the deferred-unit lists of k_render_p<true>, one per
+// XCD slice (a wave appends a unit to the list of the slice it took it
+// from; 8 counters instead of one keep the appends as spread as the takes):
+// slice x's count at defer[x * kQueueStride + kDeferCount], its list at
+// defer[kDeferList + x * kDeferSliceCap ...].  A slice with more than
+// kDeferSliceCap deferred units is re-rendered whole.  k_render_defer,
+// launched behind it on the same stream, renders them (its waves take
+// entries from the slice's defer[x * kQueueStride + kDeferTake] and count
+// themselves out on defer[kDeferDoneWord]); its last wave zeroes every count,
+// take counter and the done counter.
 constexpr int kQueueStride = 32;
 constexpr int kQueueSlots = 8;
 constexpr int kDeferCount = 0;
 constexpr int kDeferTake = 1;
-constexpr int kDeferDone = 2;
-constexpr int kDeferList = 32;
-constexpr int kDeferCap = 4096;
-constexpr size_t kQueueWords = 8 * kQueueStride + kDeferList + kDeferCap;
+constexpr int kDeferDoneWord = 8 * kQueueStride;
+constexpr int kDeferList = kDeferDoneWord + kQueueStride;
+constexpr int kDeferSliceCap = 512;
+constexpr size_t kQueueWords = 8 * kQueueStride + kDeferList + 8 * kDeferSliceCap;
 constexpr size_t kQueueBytes = kQueueWords * sizeof(uint32_t);
 struct WorkQueue {
         uint32_t *ctr;
@@ -293,52 +298,6 @@ __host__ __device__ inline void deal_slot(const TileDeal &d, int tx, int ty, int
         k = deal_blocks(d, r) * d.G * d.G + li / d.nranks;
 }
 
-// Unit order of a persistent launch: 2^sh units per 8x8-pixel tile (the 4
-// quadrants of a primary render, the 64 pixels of a config-5 launch).  When
-// this rank's tiles form an exact grid (vw columns x rows: one rank, or a
-// column count divisible by the ranks), XCD slice x is the vertical strip of
-// tile columns [x*vw/8, (x+1)*vw/8), numbered row-major inside the strip,
-// so the units one XCD runs at a time cover a compact screen region (its L2
-// serves one part of the octree).  Otherwise slice x is the contiguous
-// range queue_range() gives.  The host uses the same functions for the
-// queue bases.
-#ifndef VRT_STRIPS
-#define VRT_STRIPS 0
-#endif
-struct UnitMap {
-        int units, vw, rows, sh;
-        bool strips;
-};
-__host__ __device__ inline UnitMap unit_map(int ntx, int nty, int nranks, int tiles, int sh)
-{
-        UnitMap m;
-        m.units = tiles << sh;
-        m.vw = ntx / nranks;
-        m.rows = nty;
-        m.sh = sh;
-        m.strips = VRT_STRIPS && nranks == 1 && m.vw * nty == tiles && m.vw >= 8;
-        return m;
-}
-__host__ __device__ inline void slice_range(const UnitMap &m, int x, int &lo, int &hi)
-{
-        if (m.strips) {
-                lo = (m.rows * (x * m.vw / 8)) << m.sh;
-                hi = (m.rows * ((x + 1) * m.vw / 8)) << m.sh;
-        } else {
-                queue_range(m.units, x, lo, hi);
-        }
-}
-// unit `unit` of slice x (lo = its first unit) -> rank-local tile k << sh |
-// the unit's index inside the tile
-__host__ __device__ inline int unit_tile_sub(const UnitMap &m, int x, int unit, int lo)
-{
-        if (!m.strips)
-                return unit;
-        const int c0 = x * m.vw / 8, sw = (x + 1) * m.vw / 8 - c0;
-        const int j = (unit - lo) >> m.sh;
-        return (((j / sw) * m.vw + c0 + j % sw) << m.sh) | (unit & ((1 << m.sh) - 1));
-}
-
 // Camera + film constants for ray generation (T1), computed on the host.
 struct CamParams {
         float s[3], u[3], nf[3], e[3];  // columns of C_
@@ -408,10 +367,8 @@ struct TraceParams {
         float split_up[64];
         // split path (rec != nullptr): per-sample records of the primary
         // pass (4 x float4: hit point | hit flag, normal, albedo or sky,
-        // direct light) and the 6 cone results per sample (col[cone][slot]),
-        // tiles_this_rank*256 slots
+        // direct light), tiles_this_rank*256 slots, read by k_cones_film
         float4 *rec;
-        float *col;
 };
 
 // GPU octree build (vrt_build.hip): the host build's
@@ -463,10 +420,11 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,
                             const WorkQueue *q, hipStream_t st, int *q_waves, int slice_units[8]);
 hipError_t launch_light(const LightParams &p, hipStream_t st);
 // samp: n x 6 floats followed by room for their sorted copy (n x 6);
-// seg_start: max_seg entries (>= non-empty leaves), nseg zeroed
+// seg_start: max_seg entries (>= non-empty leaves), nseg zeroed; seg_end:
+// one entry per node (each hit leaf's run end is written)
 hipError_t launch_lm_accum(int64_t n, const uint32_t *keys_sorted, const uint32_t *vals_sorted,
                            const float *samp, uint32_t miss_key, uint32_t *seg_start, unsigned int *nseg,
-                           int64_t max_seg, LMRec *lm, hipStream_t st);
+                           int64_t max_seg, uint32_t *seg_end, LMRec *lm, hipStream_t st);
 hipError_t launch_lm_leaves(const NodeRec *nodes, int64_t nnodes, LMRec *lm, hipStream_t st);
 hipError_t launch_lm_level(const NodeRec *nodes, int64_t begin, int64_t end, LMRec *lm, hipStream_t st);
 hipError_t launch_trace(const TraceParams &p, hipStream_t st);

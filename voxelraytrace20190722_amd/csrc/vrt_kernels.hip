@@ -1515,19 +1515,18 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
         __shared__ uint2 stk[kStack * kPersistBlock];
         stage_nodes<kNS>(p.sc.mnodes, p.sc.nnodes);  // = nodes for internal nodes and the root
         const int tid = threadIdx.x, lane = tid & 63;
-        const UnitMap um = unit_map(p.ntx, p.nty, p.nranks, p.tiles_this_rank, 2);
         const int xcd = blockIdx.x & 7;
         for (int j = 0; j < (VRT_PERSIST_HELP ? 8 : 1); ++j) {
                 const int x = (xcd + j) & 7;
                 int lo, hi;
-                slice_range(um, x, lo, hi);
+                queue_range(p.tiles_this_rank * 4, x, lo, hi);
                 if (lo >= hi)
                         continue;
                 for (;;) {
                         const uint32_t u = take_unit(p.q.ctr + x * kQueueStride) - p.q.base[x];
                         if (u >= (uint32_t)(hi - lo))
                                 break;
-                        const int kq = unit_tile_sub(um, x, lo + (int)u, lo);
+                        const int kq = lo + (int)u;
 #if VRT_PHASE_STAMPS
                         const unsigned long long d_u0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1542,47 +1541,71 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
                         // a lane-0-only atomic inside this loop, and every lane
                         // stores the same word
                         if (!done) {
-                                const uint32_t d = take_unit(p.q.defer + kDeferCount);
-                                if (d < (uint32_t)kDeferCap)
-                                        p.q.defer[kDeferList + d] = (uint32_t)kq;
+                                // past the cap the slice is re-rendered whole: no more appends
+                                uint32_t *cnt = p.q.defer + x * kQueueStride + kDeferCount;
+                                const uint32_t c = __builtin_amdgcn_readfirstlane(
+                                        __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                                if (c <= (uint32_t)kDeferSliceCap) {
+                                        const uint32_t d = take_unit(cnt);
+                                        if (d < (uint32_t)kDeferSliceCap)
+                                                p.q.defer[kDeferList + x * kDeferSliceCap + d] = (uint32_t)kq;
+                                }
                         }
                 }
         }
 }
 
 // The units k_render_p<true> deferred (normally none), rendered with the
-// general march (ray_march_dispatch) by a grid as large as the persistent
-// launch's, so even a frame whose every unit was deferred runs on the whole
-// chip.  No deferred unit: every wave returns after one scalar load.
-// Otherwise the waves pull list entries (more than kDeferCap deferred units:
-// every unit of the launch; the render is deterministic, so units already
-// written are rewritten with the same values) from the take counter with
-// whole-wave atomics, and the last wave to finish resets the count and both
+// general march (ray_march_dispatch) by half as many workgroups as the
+// persistent launch (so even a frame whose every unit was deferred runs on
+// half the resident slots; a latency-bound march loses far less than half
+// its rate).  No deferred unit: every wave returns after 8 scalar loads.
+// Otherwise each wave walks the XCD slices like k_render_p (its own first),
+// taking a slice's list entries -- or, past kDeferSliceCap, every unit of
+// the slice (the render is deterministic, so units already written are
+// rewritten with the same values) -- from the slice's take counter with
+// whole-wave atomics; the last wave to finish zeroes the counts and
 // counters for the queue slot's next launch (every other wave has finished
 // reading them: its done-add follows its last, returned, take).
 __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_render_defer(RenderParams p)
 {
         __shared__ uint2 stk[kStack * kPersistBlock];
         const int tid = threadIdx.x, lane = tid & 63;
-        const uint32_t n = __builtin_amdgcn_readfirstlane(p.q.defer[kDeferCount]);
-        if (n == 0u)
+        uint32_t any = 0;
+#pragma unroll
+        for (int x = 0; x < 8; ++x)
+                any |= __builtin_amdgcn_readfirstlane(p.q.defer[x * kQueueStride + kDeferCount]);
+        if (any == 0u)
                 return;
-        const uint32_t units = (uint32_t)p.tiles_this_rank * 4u;
-        const bool all = n > (uint32_t)kDeferCap;
-        const uint32_t m = all ? units : n;
-        for (;;) {
-                const uint32_t i = take_unit(p.q.defer + kDeferTake);
-                if (i >= m)
-                        break;
-                const uint32_t unit = all ? i : __builtin_amdgcn_readfirstlane(p.q.defer[kDeferList + i]);
-                render_unit<false, false, kPersistBlock, false, false>(p, (int)(unit >> 2), (int)(unit & 3), lane,
-                                                                        stk + tid, nullptr, nullptr);
+        const int xcd = blockIdx.x & 7;
+        for (int j = 0; j < 8; ++j) {
+                const int x = (xcd + j) & 7;
+                const uint32_t n = __builtin_amdgcn_readfirstlane(p.q.defer[x * kQueueStride + kDeferCount]);
+                if (n == 0u)
+                        continue;
+                int lo, hi;
+                queue_range(p.tiles_this_rank * 4, x, lo, hi);
+                const bool all = n > (uint32_t)kDeferSliceCap;
+                const uint32_t m = all ? (uint32_t)(hi - lo) : n;
+                for (;;) {
+                        const uint32_t i = take_unit(p.q.defer + x * kQueueStride + kDeferTake);
+                        if (i >= m)
+                                break;
+                        const uint32_t unit = all ? (uint32_t)lo + i
+                                                  : __builtin_amdgcn_readfirstlane(
+                                                            p.q.defer[kDeferList + x * kDeferSliceCap + i]);
+                        render_unit<false, false, kPersistBlock, false, false>(
+                                p, (int)(unit >> 2), (int)(unit & 3), lane, stk + tid, nullptr, nullptr);
+                }
         }
-        const uint32_t fin = take_unit(p.q.defer + kDeferDone);
+        const uint32_t fin = take_unit(p.q.defer + kDeferDoneWord);
         if (fin == gridDim.x * (uint32_t)(kPersistBlock / 64) - 1u) {
-                p.q.defer[kDeferCount] = 0u;
-                p.q.defer[kDeferTake] = 0u;
-                p.q.defer[kDeferDone] = 0u;
+#pragma unroll
+                for (int x = 0; x < 8; ++x) {
+                        p.q.defer[x * kQueueStride + kDeferCount] = 0u;
+                        p.q.defer[x * kQueueStride + kDeferTake] = 0u;
+                }
+                p.q.defer[kDeferDoneWord] = 0u;
         }
 }
 
@@ -1843,20 +1866,19 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
         __shared__ uint2 stk[kStack * kSecPBlock];
         __shared__ float pts[kSecPBlock / 64][64][3];
         const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-        const UnitMap um = unit_map(p.W8 >> 3, p.H8 >> 3, p.nranks, p.units >> 6, 6);
         const int xcd = blockIdx.x & 7;
         for (int j = 0; j < 8; ++j) {
                 const int x = (xcd + j) & 7;
                 int lo, hi;
-                slice_range(um, x, lo, hi);
+                queue_range(p.units, x, lo, hi);
                 if (lo >= hi)
                         continue;
                 for (;;) {
                         const uint32_t u = take_unit(p.q.ctr + x * kQueueStride) - p.q.base[x];
                         if (u >= (uint32_t)(hi - lo))
                                 break;
-                        secondary_pixel<kR64, kAny, kSecPBlock>(p, (int64_t)unit_tile_sub(um, x, lo + (int)u, lo),
-                                                                lane, stk + tid, pts[wave]);
+                        secondary_pixel<kR64, kAny, kSecPBlock>(p, (int64_t)(lo + (int)u), lane, stk + tid,
+                                                                pts[wave]);
                 }
         }
 }
@@ -1909,10 +1931,9 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                                                   : (any ? k_secondary_p<false, true> : k_secondary_p<false, false>);
                 hipLaunchKernelGGL(kern, dim3(g), dim3(kSecPBlock), 0, st, sp);
                 *q_waves = g * (kSecPBlock / 64);
-                const UnitMap um = unit_map(rp.ntx, rp.nty, nranks, (int)mine, 6);
                 for (int x = 0; x < 8; ++x) {
                         int lo, hi;
-                        slice_range(um, x, lo, hi);
+                        queue_range((int)waves, x, lo, hi);
                         slice_units[x] = hi - lo;
                 }
                 return hipGetLastError();
@@ -2147,7 +2168,8 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                                 return e;
                         if (p.test_flags & VRT_TEST_FAIL_LAUNCH)  // test hook: fail between the two launches
                                 return hipErrorLaunchFailure;
-                        hipLaunchKernelGGL(k_render_defer, dim3(g), dim3(kPersistBlock), 0, st, p);
+                        hipLaunchKernelGGL(k_render_defer, dim3(std::max(8, (g / 2) & ~7)), dim3(kPersistBlock), 0,
+                                           st, p);
                 } else {
                         hipLaunchKernelGGL(k_render_p<false>, dim3(g), dim3(kPersistBlock), 0, st, p);
                 }
@@ -2155,10 +2177,9 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 // slice (VRT_PERSIST_HELP), or only its own XCD's (g is a
                 // multiple of 8: g/8 blocks per XCD residue)
                 *q_waves = (VRT_PERSIST_HELP ? g : g / 8) * (kPersistBlock / 64);
-                const UnitMap um = unit_map(p.ntx, p.nty, p.nranks, p.tiles_this_rank, 2);
                 for (int x = 0; x < 8; ++x) {
                         int lo, hi;
-                        slice_range(um, x, lo, hi);
+                        queue_range(p.tiles_this_rank * 4, x, lo, hi);
                         slice_units[x] = hi - lo;
                 }
                 return hipGetLastError();
@@ -2346,16 +2367,21 @@ __global__ __launch_bounds__(256) void k_lm_gather(int64_t n, const uint32_t *__
         o[2] = q[2];
 }
 
-// Start index of every run of equal (hit) leaf keys; run order is irrelevant.
+// Start index of every run of equal (hit) leaf keys (run order is
+// irrelevant) and, per leaf, the end of its run.
 __global__ __launch_bounds__(256) void k_lm_segments(int64_t n, const uint32_t *__restrict__ keys,
                                                      uint32_t miss_key, uint32_t *__restrict__ seg_start,
-                                                     unsigned int *__restrict__ nseg)
+                                                     unsigned int *__restrict__ nseg, uint32_t *__restrict__ seg_end)
 {
         const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
         if (i >= n)
                 return;
         const uint32_t leaf = keys[i];
-        if (leaf >= miss_key || (i > 0 && keys[i - 1] == leaf))
+        if (leaf >= miss_key)
+                return;
+        if (i + 1 == n || keys[i + 1] != leaf)
+                seg_end[leaf] = (uint32_t)(i + 1);
+        if (i > 0 && keys[i - 1] == leaf)
                 return;
         seg_start[atomicAdd(nseg, 1u)] = (uint32_t)i;
 }
@@ -2364,12 +2390,15 @@ __global__ __launch_bounds__(256) void k_lm_segments(int64_t n, const uint32_t *
 // order); lane 3d+c owns the running sum leaf->illum[d][c] and adds
 // clamp(dot(illum_d[d], n), 0, 1) * illum[c] sample by sample, from zero
 // (VRT/main.cc:90-95).  The 18 sums are independent, so they run side by
-// side; each stays a strictly sequential chain.
-__global__ __launch_bounds__(256) void k_lm_accum(int64_t n, const uint32_t *__restrict__ keys,
-                                                  const float *__restrict__ samp,
+// side; each stays a strictly sequential chain.  The run's end is known
+// (seg_end), so the samples' loads and coefficients are issued kLmBatch at a
+// time ahead of the chain of adds instead of one load round trip per add.
+constexpr int kLmBatch = 8;
+__global__ __launch_bounds__(256) void k_lm_accum(const float *__restrict__ samp,
+                                                  const uint32_t *__restrict__ keys,
                                                   const uint32_t *__restrict__ seg_start,
                                                   const unsigned int *__restrict__ nseg,
-                                                  LMRec *__restrict__ lm)
+                                                  const uint32_t *__restrict__ seg_end, LMRec *__restrict__ lm)
 {
         const uint32_t seg = blockIdx.x * 8 + (threadIdx.x >> 5);
         const int l = threadIdx.x & 31;
@@ -2378,12 +2407,25 @@ __global__ __launch_bounds__(256) void k_lm_accum(int64_t n, const uint32_t *__r
         const int d = l / 3, c = l % 3;
         const int64_t i0 = seg_start[seg];
         const uint32_t leaf = keys[i0];
+        const int64_t i1 = seg_end[leaf];
         const f3 dir = illum_dir(d);
         float acc = 0.f;
-        for (int64_t j = i0; j < n && keys[j] == leaf; ++j) {
-                const float *q = samp + 6 * j;  // gathered into sorted order
-                float coeff = dot(dir, mk3(q[3], q[4], q[5]));
-                coeff = clampf(coeff, 0.f, 1.f);
+        int64_t j = i0;
+        for (; j + kLmBatch <= i1; j += kLmBatch) {
+                float cf[kLmBatch], v[kLmBatch];
+#pragma unroll
+                for (int u = 0; u < kLmBatch; ++u) {
+                        const float *q = samp + 6 * (j + u);  // gathered into sorted order
+                        cf[u] = clampf(dot(dir, mk3(q[3], q[4], q[5])), 0.f, 1.f);
+                        v[u] = q[c];
+                }
+#pragma unroll
+                for (int u = 0; u < kLmBatch; ++u)
+                        acc = acc + cf[u] * v[u];
+        }
+        for (; j < i1; ++j) {
+                const float *q = samp + 6 * j;
+                const float coeff = clampf(dot(dir, mk3(q[3], q[4], q[5])), 0.f, 1.f);
                 acc = acc + coeff * q[c];
         }
         lm[leaf].illum[l] = acc;
@@ -2720,100 +2762,68 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
         }
 }
 
-// Cones: blockIdx.y = cone i, 64 consecutive sample slots per wave (the
-// same cone of neighbouring samples: coherent node reads).  cone[i][slot] =
-// cone_trace(root, cone_i, res) (VRT/voxel_octree.cc:276-311); misses skip.
-__global__ __launch_bounds__(64) void k_cones(TraceParams p, int64_t nslots)
+// Cones + film: one wave per work unit of the primary pass (its 64 sample
+// slots: 16 pixels x 4 samples, lane = 4 * pixel + sample).  A hit lane
+// marches the 6 cones one after the other (the wave marches the same cone of
+// 64 neighbouring samples at a time: coherent node reads) and sums them in
+// cone order from zero as cone_trace does (VRT/voxel_octree.cc:276-311),
+// then trace()'s get_albedo * (indirect + direct) (VRT/main.cc:22-27); a
+// miss keeps its sky colour.  The pixel's 4 samples are added in sample order
+// with cross-lane reads (Film::add(c * .25f), VRT/main.cc:121) and the
+// pixel is written once: each sample record is read once, and no per-cone
+// result goes through memory.
+__global__ __launch_bounds__(64) void k_cones_film(TraceParams p)
 {
-        const int ci = blockIdx.y;
-        const int64_t slot = (int64_t)blockIdx.x * 64 + threadIdx.x;
-        if (slot >= nslots)
-                return;
-        const float4 r0 = p.rec[4 * slot + 0];
-        if (r0.w == 0.f)
-                return;
-        const float4 r1 = p.rec[4 * slot + 1];
-        const float hx[6] = { 0.000000f, 0.000000f, 0.823639f, 0.509037f, -0.509037f, -0.823639f };
-        const float hy[6] = { 0.000000f, 0.866025f, 0.267617f, -0.700629f, -0.700629f, 0.267617f };
-        const float hz[6] = { 1.0f, 0.5f, 0.5f, 0.5f, 0.5f, 0.5f };
-        const f3 n = mk3(r1.x, r1.y, r1.z);
-        const float sg = (0.0f > n.z) ? -1.0f : 1.0f;
-        const float a0 = -1.0f / (sg + n.z);
-        const float a1 = n.x * n.y * a0;
-        const f3 t = mk3(1.0f + sg * n.x * n.x * a0, sg * a1, -sg * n.x);
-        const f3 bb = mk3(a1, sg + n.y * n.y * a0, -n.y);
-        f3 rr = mk3(0.f, 0.f, 0.f);
-        rr = rr + t * hx[ci];
-        rr = rr + bb * hy[ci];
-        rr = rr + n * hz[ci];
-        const f3 cm = cone_march(p, mk3(r0.x, r0.y, r0.z), normalize(rr));
-        float *o = p.col + 3 * ((int64_t)ci * nslots + slot);
-        o[0] = cm.x;
-        o[1] = cm.y;
-        o[2] = cm.z;
-}
-
-// Film::add(c * .25f) over the 4 samples of each pixel, in sample order,
-// into the image / tile layout of k_render; optional per-sample outputs.
-__global__ __launch_bounds__(256) void k_trace_film(TraceParams p, int64_t npix_slots)
-{
-        const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        if (g >= npix_slots)
-                return;
+        const int u = blockIdx.x;
         constexpr int kQ = 4 / VRT_RENDER_WAVES;
-        const int64_t slot0 = 4 * g;
-        const int u = (int)(slot0 / kRenderBlock);
-        const int tid0 = (int)(slot0 % kRenderBlock);
-        const int k = u / kQ;
+        if (u >= p.r.tiles_this_rank * kQ)
+                return;
+        const int lane = threadIdx.x;
+        const int64_t slot = (int64_t)u * 64 + lane;
+        const int k = u / kQ, wave = u % kQ;
         int tx, ty;
         deal_tile(tile_deal(p.r.ntx, p.r.nty, p.r.nranks), p.r.rank, k, tx, ty);
-        const int wave = (u % kQ) * VRT_RENDER_WAVES + (tid0 >> 6);
-        const int pix = (tid0 & 63) >> 2;
+        const int s = lane & 3, pix = lane >> 2;
         const int lx = (wave & 1) * 4 + (pix & 3), ly = (wave >> 1) * 4 + (pix >> 2);
         const int px = tx * 8 + lx, py = ty * 8 + ly;
-        const int64_t nslots = 4 * npix_slots;
-        const float hw[6] = { 0.25f, 0.15f, 0.15f, 0.15f, 0.15f, 0.15f };
-        float acc[3] = { 0.0f, 0.0f, 0.0f };
-        for (int s = 0; s < 4; ++s) {
-                const int64_t slot = slot0 + s;
-                const float4 r0 = p.rec[4 * slot + 0], r2 = p.rec[4 * slot + 2];
-                f3 col;
-                if (r0.w != 0.f) {
-                        // diffuse += weight_i * cone_i in cone order, from zero;
-                        // get_albedo * (indirect + direct) (VRT/main.cc:22-27)
-                        f3 diffuse = mk3(0.f, 0.f, 0.f);
-                        for (int i = 0; i < 6; ++i) {
-                                const float *q = p.col + 3 * ((int64_t)i * nslots + slot);
-                                diffuse = diffuse + mk3(q[0], q[1], q[2]) * hw[i];
-                        }
-                        const float4 r3 = p.rec[4 * slot + 3];
-                        const f3 lsum = diffuse + mk3(r3.x, r3.y, r3.z);
-                        col = mk3(r2.x * lsum.x, r2.y * lsum.y, r2.z * lsum.z);
-                } else {
-                        col = mk3(r2.x, r2.y, r2.z);
-                }
-                const float c[3] = { col.x, col.y, col.z };
-                const f3 cq = col * .25f;
-                acc[0] += cq.x;
-                acc[1] += cq.y;
-                acc[2] += cq.z;
-                const size_t si = ((size_t)py * p.r.cam.nx + px) * 4 + s;
-                if (p.r.so.hit)
-                        p.r.so.hit[si] = r0.w != 0.f ? 1 : 0;
-                if (p.r.so.rgb) {
-                        p.r.so.rgb[3 * si + 0] = c[0];
-                        p.r.so.rgb[3 * si + 1] = c[1];
-                        p.r.so.rgb[3 * si + 2] = c[2];
-                }
+        const float4 r0 = p.rec[4 * slot + 0], r2 = p.rec[4 * slot + 2];
+        f3 col;
+        if (r0.w != 0.f) {
+                const float4 r1 = p.rec[4 * slot + 1], r3 = p.rec[4 * slot + 3];
+                const f3 diffuse = cone_trace_isect(p, mk3(r0.x, r0.y, r0.z), mk3(r1.x, r1.y, r1.z));
+                const f3 lsum = diffuse + mk3(r3.x, r3.y, r3.z);
+                col = mk3(r2.x * lsum.x, r2.y * lsum.y, r2.z * lsum.z);
+        } else {
+                col = mk3(r2.x, r2.y, r2.z);
         }
-        float *o;
-        if (p.r.image_layout)
-                o = p.r.out + ((size_t)py * p.r.cam.nx + px) * 3;
-        else
-                o = p.r.out + ((size_t)k * 64 + ly * 8 + lx) * 3;
-        o[0] = acc[0];
-        o[1] = acc[1];
-        o[2] = acc[2];
+        const size_t si = ((size_t)py * p.r.cam.nx + px) * 4 + s;
+        if (p.r.so.hit)
+                p.r.so.hit[si] = r0.w != 0.f ? 1 : 0;
+        if (p.r.so.rgb) {
+                p.r.so.rgb[3 * si + 0] = col.x;
+                p.r.so.rgb[3 * si + 1] = col.y;
+                p.r.so.rgb[3 * si + 2] = col.z;
+        }
+        const f3 cq = col * .25f;
+        const int l0 = lane & ~3;
+        float acc[3] = { 0.0f, 0.0f, 0.0f };
+        const float cv[3] = { cq.x, cq.y, cq.z };
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                        acc[q] += __shfl(cv[q], l0 + j, 64);
+        }
+        if (s == 0) {
+                float *o;
+                if (p.r.image_layout)
+                        o = p.r.out + ((size_t)py * p.r.cam.nx + px) * 3;
+                else
+                        o = p.r.out + ((size_t)k * 64 + ly * 8 + lx) * 3;
+                o[0] = acc[0];
+                o[1] = acc[1];
+                o[2] = acc[2];
+        }
 }
 
 __global__ void k_iota(uint32_t *v, int64_t n)
@@ -2834,7 +2844,7 @@ hipError_t launch_light(const LightParams &p, hipStream_t st)
 
 hipError_t launch_lm_accum(int64_t n, const uint32_t *keys_sorted, const uint32_t *vals_sorted,
                            const float *samp, uint32_t miss_key, uint32_t *seg_start, unsigned int *nseg,
-                           int64_t max_seg, LMRec *lm, hipStream_t st)
+                           int64_t max_seg, uint32_t *seg_end, LMRec *lm, hipStream_t st)
 {
         if (n <= 0)
                 return hipSuccess;
@@ -2843,10 +2853,11 @@ hipError_t launch_lm_accum(int64_t n, const uint32_t *keys_sorted, const uint32_
         float *sorted = const_cast<float *>(samp) + 6 * n;
         const unsigned g = (unsigned)((n + 255) / 256);
         hipLaunchKernelGGL(k_lm_gather, dim3(g), dim3(256), 0, st, n, vals_sorted, samp, sorted);
-        hipLaunchKernelGGL(k_lm_segments, dim3(g), dim3(256), 0, st, n, keys_sorted, miss_key, seg_start, nseg);
+        hipLaunchKernelGGL(k_lm_segments, dim3(g), dim3(256), 0, st, n, keys_sorted, miss_key, seg_start, nseg,
+                           seg_end);
         if (max_seg > 0)
-                hipLaunchKernelGGL(k_lm_accum, dim3((unsigned)((max_seg + 7) / 8)), dim3(256), 0, st, n, keys_sorted,
-                                   sorted, seg_start, nseg, lm);
+                hipLaunchKernelGGL(k_lm_accum, dim3((unsigned)((max_seg + 7) / 8)), dim3(256), 0, st, sorted,
+                                   keys_sorted, seg_start, nseg, seg_end, lm);
         return hipGetLastError();
 }
 
@@ -2878,9 +2889,7 @@ hipError_t launch_trace(const TraceParams &p, hipStream_t st)
         }
         const int64_t nslots = (int64_t)p.r.tiles_this_rank * 256;
         hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace_prim<true> : k_trace_prim<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
-        hipLaunchKernelGGL(k_cones, dim3((unsigned)((nslots + 63) / 64), 6), dim3(64), 0, st, p, nslots);
-        hipLaunchKernelGGL(k_trace_film, dim3((unsigned)((nslots / 4 + 255) / 256)), dim3(256), 0, st, p,
-                           nslots / 4);
+        hipLaunchKernelGGL(k_cones_film, dim3((unsigned)(nslots / 64)), dim3(64), 0, st, p);
         return hipGetLastError();
 }
 
