@@ -568,3 +568,20 @@ def test_maximum_depth_matches_oracle(depth):
     for key in ("hit", "tri", "voxel"):
         assert np.array_equal(g[key], o[key]), key
     assert np.array_equal(bits(g["hit_p"]), bits(o["hit_p"]))
+
+
+def test_trace_main_frame_256_matches_oracle():
+    """The reference main() frame at 256x256 on the full sponza-proxy
+    (depth 6, light map 512^2): light map, filter and the cone-traced image
+    bit-exact vs the oracle's canonical order -- every cone step of 262,144
+    samples x 6 cones through the descent tables (TraceParams::ctab)."""
+    sd = vrt.SceneData.proxy(1.0, 1)
+    tree = vrt.VoxelOctree(sd, 6)
+    osc = po.Scene(sd, 6)
+    hits = tree.lightmap(vrt.Camera(*LIGHT), vrt.Film(1, 1, 512, 512))
+    assert hits == osc.lightmap(po.camera(*LIGHT), 1.0, 1.0, 512, 512, nthreads=16) > 0
+    res = tree.min_voxel(6)
+    cam = (vrt.to_radian(90), (1.0, 1.3, -0.2), (0.0, 0.4, 0.0), (0.0, 1.0, 0.0))
+    rgb = tree.render_trace(vrt.Camera(*cam), vrt.Film(1, 1, 256, 256), res)
+    orgb = osc.render_trace(po.camera(*cam), 1.0, 1.0, 256, 256, res, nthreads=16, samples=False)
+    assert np.array_equal(bits(rgb), bits(orgb))

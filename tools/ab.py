@@ -40,7 +40,8 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--detail", type=float, default=1.0)
-    ap.add_argument("--mode", default="primary", choices=["primary", "secondary"])
+    ap.add_argument("--mode", default="primary", choices=["primary", "secondary", "trace"])
+    ap.add_argument("--light-n", type=int, default=2048, help="--mode trace: light film side (VRT/main.cc:79)")
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--no-check", action="store_true", help="timing-only variants (images may differ)")
     ap.add_argument("--ranks", type=int, default=1,
@@ -60,6 +61,8 @@ def main():
         scenes.append(h)
     info = _ffi.SceneInfo()
     libs[0].vrt_scene_info(scenes[0], C.byref(info))
+    if a.mode == "trace":
+        return trace_ab(a, libs, scenes, film)
     cams = []
     for i in range(a.poses):
         fov, eye, spot, up = vrt.sweep_pose(info.root_min[:], info.root_max[:], i, a.poses)
@@ -139,6 +142,58 @@ def main():
                                     "speedup": round(float(base / np.median(t)), 3),
                                     "mrays": round(a.width * a.height * 4 / np.median(t) / 1e3, 1)}
     print(json.dumps(out, indent=1))
+
+
+def mkcam(L, fov, eye, spot, up):
+    cam = _ffi.Camera()
+    f3 = lambda v: np.ascontiguousarray(np.asarray(v, np.float32))  # noqa: E731
+    e, s_, u = f3(eye), f3(spot), f3(up)
+    L.vrt_camera_init(fov, e.ctypes.data_as(_ffi.f32p), s_.ctypes.data_as(_ffi.f32p), u.ctypes.data_as(_ffi.f32p),
+                      0.0, vrt.FLT_MAX, C.byref(cam))
+    return cam
+
+
+def trace_ab(a, libs, scenes, film):
+    """--mode trace: the reference main() frame's cone-traced render
+    (vrt_render_trace_device, light map built once per variant), timed per
+    launch; images must be bit-identical across variants."""
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream(dev)
+    light = mkcam(libs[0], vrt.to_radian(60), (1, 10, 1), (0, 0, 0), (0, 1, 0))
+    lfilm = _ffi.Film(1.0, 1.0, a.light_n, a.light_n)
+    view = mkcam(libs[0], vrt.to_radian(90), (1.0, 1.3, -0.2), (0.0, 0.4, 0.0), (0.0, 1.0, 0.0))
+    for L, h in zip(libs, scenes):
+        hits = C.c_int64()
+        assert L.vrt_lightmap_build(h, C.byref(light), C.byref(lfilm), C.byref(hits)) == 0, L.vrt_last_error()
+    imgs = [torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev) for _ in libs]
+    times = {p: [] for p in a.libs}
+    ref = None
+    for r in range(a.rounds + 1):
+        for vi, (L, h, p) in enumerate(zip(libs, scenes, a.libs)):
+            evs = []
+            for _ in range(4):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                rc = L.vrt_render_trace_device(h, C.byref(view), C.byref(film), 0.0, 0, 1, 1,
+                                               C.c_void_p(imgs[vi].data_ptr()), C.c_void_p(st.cuda_stream))
+                assert rc == 0, L.vrt_last_error()
+                e1.record(st)
+                evs.append((e0, e1))
+            torch.cuda.synchronize()
+            if r == 0:
+                im = imgs[vi].cpu().numpy().view(np.uint32)
+                if ref is None:
+                    ref = im
+                elif not a.no_check and not np.array_equal(im, ref):
+                    raise SystemExit(f"variant {p} differs from baseline {a.libs[0]}")
+            else:
+                times[p].append(sum(s_.elapsed_time(e_) for s_, e_ in evs) / len(evs))
+    base = np.median(times[a.libs[0]])
+    print(json.dumps({os.path.basename(p): {"median_ms": round(float(np.median(t)), 4),
+                                            "min_ms": round(float(np.min(t)), 4),
+                                            "speedup": round(float(base / np.median(t)), 3)}
+                      for p, t in times.items()}, indent=1))
 
 
 if __name__ == "__main__":

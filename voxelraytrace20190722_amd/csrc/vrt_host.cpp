@@ -1906,6 +1906,58 @@ static int trace_scratch(vrt_scene *s, const TraceParams &tp, TraceParams *out, 
         return VRT_OK;
 }
 
+// The cone march's split level as a function of the diameter
+// (TraceParams::split_bound): S(diam) = split_level_of(fl(maxdist / diam))
+// -- the kernels' own rule on the correctly rounded quotient, which the host
+// division reproduces -- is non-increasing in diam, so bound[k] = the
+// largest float diam with S(diam) >= k, found by bisection over the float
+// bit patterns (monotone in value for positive floats).
+static int split_level_host(float x, const float *up)
+{
+        uint32_t u;
+        std::memcpy(&u, &x, 4);
+        const int e = (int)(u >> 23) - 127;
+        if (e >= 63)
+                return e;
+        return x >= up[e] ? e + 1 : e;
+}
+
+static void split_bounds(float maxdist, const float *up, float *bound)
+{
+        static thread_local float last_max = -1.f;
+        static thread_local float last[64];
+        if (maxdist == last_max) {
+                std::memcpy(bound, last, sizeof last);
+                return;
+        }
+        bound[0] = maxdist;
+        auto S = [&](uint32_t bits) {
+                float d;
+                std::memcpy(&d, &bits, 4);
+                volatile float q = maxdist / d;  // one correctly rounded division, as on the device
+                return split_level_host(q, up);
+        };
+        uint32_t top;
+        std::memcpy(&top, &maxdist, 4);
+        for (int k = 1; k < 64; ++k) {
+                if (!(maxdist > 0.f) || !std::isfinite(maxdist) || S(1u) < k) {  // not even the least diameter
+                        bound[k] = 0.f;
+                        continue;
+                }
+                uint32_t lo = 1u, hi = top;  // S(lo) >= k; find the largest bits with S >= k
+                while (lo < hi) {
+                        const uint32_t mid = lo + (hi - lo + 1) / 2;
+                        if (S(mid) >= k)
+                                lo = mid;
+                        else
+                                hi = mid - 1;
+                }
+                std::memcpy(&bound[k], &lo, 4);
+        }
+        last_max = maxdist;
+        std::memcpy(last, bound, sizeof last);
+}
+
 static void fill_trace_params(vrt_scene *s, const vrt_camera *cam, const vrt_film *film, float min_voxel,
                               int rank, int nranks, TraceParams *tp)
 {
@@ -1922,6 +1974,7 @@ static void fill_trace_params(vrt_scene *s, const vrt_camera *cam, const vrt_fil
                           s->info.root_max[2] - s->info.root_min[2]);
         tp->maxdist = length(sz);
         std::memcpy(tp->split_up, split_table(), sizeof tp->split_up);
+        split_bounds(tp->maxdist, tp->split_up, tp->split_bound);
 }
 
 extern "C" int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam, const vrt_film *film,

@@ -365,6 +365,12 @@ struct TraceParams {
         const uint32_t *lm_bad;    // != 0: some illum is not finite (exact slow path)
         float mindist, maxdist;
         float split_up[64];
+        // split_bound[k] (k = 1..63) = the largest cone diameter whose split
+        // level (int)log2f(maxdist / diam) -- split_level_of(fl(maxdist /
+        // diam)) -- is >= k (0 if none): the level is non-increasing in diam,
+        // so it is the count of bounds >= diam, kept by a cursor as a cone's
+        // diameter grows instead of a division per step
+        float split_bound[64];
         // split path (rec != nullptr): per-sample records of the primary
         // pass (4 x float4: hit point | hit flag, normal, albedo or sky,
         // direct light), tiles_this_rank*256 slots, read by k_cones_film

@@ -2543,12 +2543,24 @@ __device__ __forceinline__ f3 cone_march_fast(const TraceParams &p, f3 o, f3 d)
         float dist = p.mindist;
         float opacity = 0.f;
         f3 diffuse = mk3(0.f, 0.f, 0.f);
+        // the split level of the current diameter (non-increasing as the
+        // diameter grows: TraceParams::split_bound), and its bound
+        int level = -1;
+        float bound = 0.f;
         for (int guard = 0; dist < p.maxdist && opacity < 1.f && guard < (1 << 16); ++guard) {
                 const f3 pt = o + d * dist;
                 const float diam = std_max(p.mindist, aperture * 2.f * dist);
                 if (p.maxdist < diam)
                         break;
-                int split = split_level_of(p.maxdist / diam, p.split_up);
+                if (level < 0) {  // first step: the reference's division once
+                        level = min(split_level_of(p.maxdist / diam, p.split_up), 63);  // >= 63: below any node
+                        bound = p.split_bound[level];
+                }
+                while (level > 0 && diam > bound) {
+                        --level;
+                        bound = p.split_bound[level];
+                }
+                int split = level;
                 uint32_t ni = 0;
                 float4 c = p.cc[0];
                 uint32_t a = __float_as_uint(c.w);
