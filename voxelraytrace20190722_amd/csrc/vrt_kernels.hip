@@ -1337,7 +1337,16 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         };
         const CamParams &c = p.cam;
         int tx, ty;
-        deal_tile(tile_deal(p.ntx, p.nty, p.nranks), p.rank, k, tx, ty);
+        {
+                // the deal's sizes pass through an opaque copy per unit, so
+                // the divisions they feed are redone per unit (a few scalar
+                // instructions) rather than hoisted as loop invariants that
+                // hold SGPRs -- and spill -- across every march
+                int ntx = p.ntx, nty = p.nty, nr = p.nranks, rk = p.rank;
+                if (!kSamples)
+                        asm volatile("" : "+s"(ntx), "+s"(nty), "+s"(nr), "+s"(rk));
+                deal_tile(tile_deal(ntx, nty, nr), rk, k, tx, ty);
+        }
         ty += p.ty0;
         // pixel, sample and Camera::gen_rays4 direction (VRT/camera.cc:95-112)
         // of lane l
@@ -1348,12 +1357,14 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                 ly = (wave >> 1) * 4 + (pix >> 2);
                 px = tx * 8 + lx;
                 py = ty * 8 + ly;
-                return camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py, sample_x(s), sample_y(s));
+                int nx = c.nx, ny = c.ny;  // opaque per unit, as the deal's sizes above
+                if (!kSamples)
+                        asm volatile("" : "+s"(nx), "+s"(ny));
+                return camera_dir(c.s, c.u, c.nf, c.e, c.z, nx, ny, px, py, sample_x(s), sample_y(s));
         };
         int px, py, s, lx, ly;
         f3 dn = sample_of(lane_now(), px, py, s, lx, ly);
-        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
-                                 dn, c.tmin, c.tmax);
+        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]), dn, c.tmin, c.tmax);
 
         MarchResult m;
         if (kFastOnly) {
@@ -1413,8 +1424,8 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
 #pragma unroll
-                for (int q = 0; q < 3; ++q)
-                        acc[q] += __shfl(cv[q], l0 + j, 64);
+                for (int q = 0; q < 3; ++q)  // lane l0 + j's value (a wave64 permute by our own lane id)
+                        acc[q] += __int_as_float(__builtin_amdgcn_ds_bpermute((l0 + j) << 2, __float_as_int(cv[q])));
         }
         if (s == 0) {
                 float *o;
@@ -1776,11 +1787,15 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
         // this rank's tile k / 64 (the 8x8-pixel tiles dealt as the primary
         // render's, tile_deal), pixel k % 64 of it, row-major
-        const TileDeal dl = tile_deal(p.W8 >> 3, p.H8 >> 3, p.nranks);
-        if ((k >> 6) >= (int64_t)deal_count(dl, p.rank))
+        // the deal's sizes pass through an opaque copy per pixel (see
+        // render_unit): its divisions are redone, not held in SGPRs
+        int ntx = p.W8 >> 3, nty = p.H8 >> 3, nr = p.nranks, rk = p.rank;
+        asm volatile("" : "+s"(ntx), "+s"(nty), "+s"(nr), "+s"(rk));
+        const TileDeal dl = tile_deal(ntx, nty, nr);
+        if ((k >> 6) >= (int64_t)deal_count(dl, rk))
                 return;
         int tx, ty;
-        deal_tile(dl, p.rank, (int)(k >> 6), tx, ty);
+        deal_tile(dl, rk, (int)(k >> 6), tx, ty);
         const int px = tx * 8 + (int)(k & 7), py = ty * 8 + (int)((k >> 3) & 7);
         const int64_t pix = (int64_t)py * p.W8 + px;
         const float *pr = p.prim + 8 * pix;
