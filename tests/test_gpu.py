@@ -367,9 +367,9 @@ def test_secondary_occlusion_walk_matches_ordered_walk(proxy_small, depth):
 @pytest.mark.parametrize("nx,ny,nranks", [(72, 40, 3), (512, 40, 8)])
 def test_secondary_rank_partition_sums_to_image(proxy_small, nx, ny, nranks):
     """Each rank writes exactly the pixels of its 8x8 tiles (dist.py
-    secondary_mask); the parts sum to the single-rank image.  512 px / 8
-    ranks: every rank's tiles form an exact grid 8 tiles wide, so the
-    persistent kernel's XCD strips are in use."""
+    secondary_mask); the parts sum to the single-rank image.  72x40 / 3
+    ranks: ragged edge strips dealt tile by tile; 512x40 / 8 ranks: whole
+    4x4-tile blocks with rank 0 dealt the lighter share (include/vrt.h)."""
     import torch
     from voxelraytrace20190722_amd import dist as vd
     tree = vrt.VoxelOctree(proxy_small, 6)

@@ -567,7 +567,18 @@ __device__ __forceinline__ void mt_record(const float4 q0, const float4 q1, cons
         const double det = e1x * px + e1y * py + e1z * pz;
         if (!(det > 0.000001) && !(det < -0.000001))
                 return;  // parallel
-        const double tx = (double)r.o.x - v0x, ty = (double)r.o.y - v0y, tz = (double)r.o.z - v0z;
+#ifndef VRT_MT_RECVT
+#define VRT_MT_RECVT 1
+#endif
+        // small-leaf scenes: the origin is widened per record instead of
+        // holding 6 VGPRs of doubles across the march (part of what lets the
+        // persistent render run 6 waves per SIMD without spilling in its
+        // advance loop; +3 % per frame); large-leaf scenes keep it hoisted
+        // (their leaf loop dominates)
+        float rox = r.o.x, roy = r.o.y, roz = r.o.z;
+        if (VRT_MT_RECVT && !kR64)
+                asm volatile("" : "+v"(rox), "+v"(roy), "+v"(roz));
+        const double tx = (double)rox - v0x, ty = (double)roy - v0y, tz = (double)roz - v0z;
         const double uu = tx * px + ty * py + tz * pz;
         const bool pos = det > 0.000001;
 #ifndef VRT_LEAF_SIGNFOLD
@@ -1511,7 +1522,7 @@ constexpr int kPersistBlock = 256;
 // grid of whole XCD rounds).
 constexpr int kCollectiveReserve = 32;
 #ifndef VRT_PERSIST_WAVES_PER_EU
-#define VRT_PERSIST_WAVES_PER_EU 5
+#define VRT_PERSIST_WAVES_PER_EU 6
 #endif
 #ifndef VRT_PERSIST_HELP
 #define VRT_PERSIST_HELP 1
