@@ -1357,6 +1357,11 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                 if (!kSamples)
                         asm volatile("" : "+s"(ntx), "+s"(nty), "+s"(nr), "+s"(rk));
                 deal_tile(tile_deal(ntx, nty, nr), rk, k, tx, ty);
+                // the tile is wave-uniform: keep it in SGPRs (the deal's
+                // divisions may run on the VALU), not in VGPRs held -- and
+                // spilled -- across the march
+                tx = __builtin_amdgcn_readfirstlane(tx);
+                ty = __builtin_amdgcn_readfirstlane(ty);
         }
         ty += p.ty0;
         // pixel, sample and Camera::gen_rays4 direction (VRT/camera.cc:95-112)
@@ -1368,10 +1373,15 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                 ly = (wave >> 1) * 4 + (pix >> 2);
                 px = tx * 8 + lx;
                 py = ty * 8 + ly;
-                int nx = c.nx, ny = c.ny;  // opaque per unit, as the deal's sizes above
+                // opaque per unit, as the deal's sizes above: the film size and
+                // the camera terms that are the same for every ray (nf * z, e *
+                // 0) are recomputed per unit, not held in VGPRs across marches
+                int nx = c.nx, ny = c.ny;
+                float nf[3] = { c.nf[0], c.nf[1], c.nf[2] }, e[3] = { c.e[0], c.e[1], c.e[2] }, z = c.z;
                 if (!kSamples)
-                        asm volatile("" : "+s"(nx), "+s"(ny));
-                return camera_dir(c.s, c.u, c.nf, c.e, c.z, nx, ny, px, py, sample_x(s), sample_y(s));
+                        asm volatile("" : "+s"(nx), "+s"(ny), "+s"(nf[0]), "+s"(nf[1]), "+s"(nf[2]), "+s"(e[0]),
+                                     "+s"(e[1]), "+s"(e[2]), "+s"(z));
+                return camera_dir(c.s, c.u, nf, e, z, nx, ny, px, py, sample_x(s), sample_y(s));
         };
         int px, py, s, lx, ly;
         f3 dn = sample_of(lane_now(), px, py, s, lx, ly);
