@@ -1550,15 +1550,14 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
         const int xcd = blockIdx.x & 7;
         for (int j = 0; j < (VRT_PERSIST_HELP ? 8 : 1); ++j) {
                 const int x = (xcd + j) & 7;
-                int lo, hi;
-                queue_range(p.tiles_this_rank * 4, x, lo, hi);
-                if (lo >= hi)
+                const int units = p.tiles_this_rank * 4, n = slice_size(units, x, VRT_SLICE_CHUNK);
+                if (n <= 0)
                         continue;
                 for (;;) {
                         const uint32_t u = take_unit(p.q.ctr + x * kQueueStride) - p.q.base[x];
-                        if (u >= (uint32_t)(hi - lo))
+                        if (u >= (uint32_t)n)
                                 break;
-                        const int kq = lo + (int)u;
+                        const int kq = slice_unit(units, x, (int)u, VRT_SLICE_CHUNK);
 #if VRT_PHASE_STAMPS
                         const unsigned long long d_u0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1615,15 +1614,14 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
                 const uint32_t n = __builtin_amdgcn_readfirstlane(p.q.defer[x * kQueueStride + kDeferCount]);
                 if (n == 0u)
                         continue;
-                int lo, hi;
-                queue_range(p.tiles_this_rank * 4, x, lo, hi);
+                const int units = p.tiles_this_rank * 4;
                 const bool all = n > (uint32_t)kDeferSliceCap;
-                const uint32_t m = all ? (uint32_t)(hi - lo) : n;
+                const uint32_t m = all ? (uint32_t)slice_size(units, x, VRT_SLICE_CHUNK) : n;
                 for (;;) {
                         const uint32_t i = take_unit(p.q.defer + x * kQueueStride + kDeferTake);
                         if (i >= m)
                                 break;
-                        const uint32_t unit = all ? (uint32_t)lo + i
+                        const uint32_t unit = all ? (uint32_t)slice_unit(units, x, (int)i, VRT_SLICE_CHUNK)
                                                   : __builtin_amdgcn_readfirstlane(
                                                             p.q.defer[kDeferList + x * kDeferSliceCap + i]);
                         render_unit<false, false, kPersistBlock, false, false>(
@@ -1905,16 +1903,16 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
         const int xcd = blockIdx.x & 7;
         for (int j = 0; j < 8; ++j) {
                 const int x = (xcd + j) & 7;
-                int lo, hi;
-                queue_range(p.units, x, lo, hi);
-                if (lo >= hi)
+                const int n = slice_size(p.units, x, VRT_SEC_SLICE_CHUNK);
+                if (n <= 0)
                         continue;
                 for (;;) {
                         const uint32_t u = take_unit(p.q.ctr + x * kQueueStride) - p.q.base[x];
-                        if (u >= (uint32_t)(hi - lo))
+                        if (u >= (uint32_t)n)
                                 break;
-                        secondary_pixel<kR64, kAny, kSecPBlock>(p, (int64_t)(lo + (int)u), lane, stk + tid,
-                                                                pts[wave]);
+                        secondary_pixel<kR64, kAny, kSecPBlock>(
+                                p, (int64_t)slice_unit(p.units, x, (int)u, VRT_SEC_SLICE_CHUNK), lane, stk + tid,
+                                pts[wave]);
                 }
         }
 }
@@ -1967,11 +1965,8 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                                                   : (any ? k_secondary_p<false, true> : k_secondary_p<false, false>);
                 hipLaunchKernelGGL(kern, dim3(g), dim3(kSecPBlock), 0, st, sp);
                 *q_waves = g * (kSecPBlock / 64);
-                for (int x = 0; x < 8; ++x) {
-                        int lo, hi;
-                        queue_range((int)waves, x, lo, hi);
-                        slice_units[x] = hi - lo;
-                }
+                for (int x = 0; x < 8; ++x)
+                        slice_units[x] = slice_size((int)waves, x, VRT_SEC_SLICE_CHUNK);
                 return hipGetLastError();
         }
         void (*kern)(SecondaryParams) = w ? (any ? k_secondary<true, true> : k_secondary<true, false>)
@@ -2213,11 +2208,8 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 // slice (VRT_PERSIST_HELP), or only its own XCD's (g is a
                 // multiple of 8: g/8 blocks per XCD residue)
                 *q_waves = (VRT_PERSIST_HELP ? g : g / 8) * (kPersistBlock / 64);
-                for (int x = 0; x < 8; ++x) {
-                        int lo, hi;
-                        queue_range(p.tiles_this_rank * 4, x, lo, hi);
-                        slice_units[x] = hi - lo;
-                }
+                for (int x = 0; x < 8; ++x)
+                        slice_units[x] = slice_size(p.tiles_this_rank * 4, x, VRT_SLICE_CHUNK);
                 return hipGetLastError();
         }
         // round the grid up to a multiple of 8 (one slot per XCD)
