@@ -83,27 +83,37 @@ def short_name(kn):
 
 
 def pmc_per_kernel(out_dir, steps):
-    """Per-frame counter totals per kernel (short name) over every dispatch
-    in the rocprofv3 *counter_collection.csv files under out_dir (the child
-    runs warm-up 0, so every dispatch belongs to one of the `steps` frames),
-    plus dispatch counts and launch geometry."""
+    """Per-frame counter totals per kernel (short name) over the timed
+    frames' dispatches in the rocprofv3 *counter_collection.csv files under
+    out_dir (one file per pass), plus dispatches per frame and launch
+    geometry.  The child runs warm-up 0, but a mode may launch a kernel
+    before its timed region (config 5 renders each pose once to count its
+    rays): of a kernel's n dispatches in a pass, the last
+    floor(n / steps) * steps (dispatch ids are in launch order) are the
+    timed frames' and the earlier ones are dropped."""
     import csv
-    rows = []
+    tot, disp, meta = {}, {}, {}
     for root, _, files in os.walk(out_dir):
         for f in files:
-            if f.endswith("counter_collection.csv"):
-                rows += list(csv.DictReader(open(os.path.join(root, f))))
-    tot, disp, meta = {}, {}, {}
-    for r in rows:
-        kn = short_name(r["Kernel_Name"])
-        t = tot.setdefault(kn, {})
-        t[r["Counter_Name"]] = t.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-        disp.setdefault(kn, set()).add(int(r["Dispatch_Id"]))
-        meta[kn] = {"kernel": r["Kernel_Name"], "grid": int(r["Grid_Size"]), "wg": int(r["Workgroup_Size"]),
-                    "lds": int(r["LDS_Block_Size"]), "vgpr": int(r["VGPR_Count"]),
-                    "sgpr": int(r["SGPR_Count"]), "scratch": int(r["Scratch_Size"])}
-    return ({k: {c: v / steps for c, v in t.items()} for k, t in tot.items()},
-            {k: len(v) / steps for k, v in disp.items()}, meta)
+            if not f.endswith("counter_collection.csv"):
+                continue
+            by_k = {}
+            for r in csv.DictReader(open(os.path.join(root, f))):
+                kn = short_name(r["Kernel_Name"])
+                by_k.setdefault(kn, []).append(r)
+                meta[kn] = {"kernel": r["Kernel_Name"], "grid": int(r["Grid_Size"]), "wg": int(r["Workgroup_Size"]),
+                            "lds": int(r["LDS_Block_Size"]), "vgpr": int(r["VGPR_Count"]),
+                            "sgpr": int(r["SGPR_Count"]), "scratch": int(r["Scratch_Size"])}
+            for kn, rows in by_k.items():
+                ids = sorted({int(r["Dispatch_Id"]) for r in rows})
+                keep = len(ids) // steps * steps if len(ids) >= steps else len(ids)
+                kept = set(ids[len(ids) - keep:])
+                t = tot.setdefault(kn, {})
+                for r in rows:
+                    if int(r["Dispatch_Id"]) in kept:
+                        t[r["Counter_Name"]] = t.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                disp[kn] = keep / steps
+    return ({k: {c: v / steps for c, v in t.items()} for k, t in tot.items()}, disp, meta)
 
 
 def pmc_means(out_dir, kernel_prefix, steps):
