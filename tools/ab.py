@@ -9,6 +9,7 @@ usage: tools/ab.py lib1.so lib2.so ... [--rounds 6] [--width 1920 --height 1080 
 import argparse
 import ctypes as C
 import json
+import time
 import os
 import sys
 
@@ -167,9 +168,17 @@ def trace_ab(a, libs, scenes, film):
         assert L.vrt_lightmap_build(h, C.byref(light), C.byref(lfilm), C.byref(hits)) == 0, L.vrt_last_error()
     imgs = [torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev) for _ in libs]
     times = {p: [] for p in a.libs}
+    ltimes = {p: [] for p in a.libs}
     ref = None
     for r in range(a.rounds + 1):
         for vi, (L, h, p) in enumerate(zip(libs, scenes, a.libs)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            hits = C.c_int64()
+            assert L.vrt_lightmap_build(h, C.byref(light), C.byref(lfilm), C.byref(hits)) == 0, L.vrt_last_error()
+            torch.cuda.synchronize()
+            if r > 0:
+                ltimes[p].append((time.perf_counter() - t0) * 1e3)
             evs = []
             for _ in range(4):
                 e0 = torch.cuda.Event(enable_timing=True)
@@ -190,9 +199,12 @@ def trace_ab(a, libs, scenes, film):
             else:
                 times[p].append(sum(s_.elapsed_time(e_) for s_, e_ in evs) / len(evs))
     base = np.median(times[a.libs[0]])
+    lbase = np.median(ltimes[a.libs[0]])
     print(json.dumps({os.path.basename(p): {"median_ms": round(float(np.median(t)), 4),
                                             "min_ms": round(float(np.min(t)), 4),
-                                            "speedup": round(float(base / np.median(t)), 3)}
+                                            "speedup": round(float(base / np.median(t)), 3),
+                                            "lightmap_wall_ms": round(float(np.median(ltimes[p])), 4),
+                                            "lightmap_speedup": round(float(lbase / np.median(ltimes[p])), 3)}
                       for p, t in times.items()}, indent=1))
 
 

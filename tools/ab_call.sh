@@ -4,7 +4,7 @@
 # first's).  Variants are built on the CPU beforehand with
 #   make variant NAME=<name> DEFS="-D..."       (kernels only)
 #   make fullvariant NAME=<name> DEFS="-D..."   (kernels + host side)
-# usage: tools/ab_call.sh [--sets d8,d9,4k,sec,r8] NAME1 NAME2 ...
+# usage: tools/ab_call.sh [--sets d8,d9,4k,sec,r8,d6,tr] NAME1 NAME2 ...
 #        (build/variants/libvrt_NAME.so; "head" = the in-tree libvrt.so)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -22,6 +22,7 @@ for s in ${sets//,/ }; do
     4k)  steps+=("ab_4k|300|python -u tools/ab.py $L --width 3840 --height 2160 --depth 9 --rounds 4") ;;
     sec) steps+=("ab_sec|400|python -u tools/ab.py $L --mode secondary --poses 8 --rounds 3") ;;
     r8)  steps+=("ab_r8|300|python -u tools/ab.py $L --ranks 8 --rounds 4") ;;
+    tr)  steps+=("ab_tr|300|python -u tools/ab.py $L --mode trace --rounds 4") ;;
     d6)  steps+=("ab_d6|300|python -u tools/ab.py $L --depth 6 --rounds 4") ;;
     *) echo "unknown set $s"; exit 2 ;;
   esac

@@ -2322,15 +2322,27 @@ __device__ __forceinline__ f3 illum_dir(int i)
         return mk3(ax == 0 ? v : 0.f, ax == 1 ? v : 0.f, ax == 2 ? v : 0.f);
 }
 
-// XCD-aware 8x8-pixel tile of this block and this lane's pixel / sample
-// (the k_render mapping).  Returns false for padding blocks.
-__device__ __forceinline__ bool tile_lane(const RenderParams &p, int &k, int &px, int &py,
+#ifndef VRT_TRACE_WAVES_PER_EU
+#define VRT_TRACE_WAVES_PER_EU 1
+#endif
+
+// Grid of the light / trace passes: one one-wave block per work unit,
+// rounded up to 8 blocks.  (Looping blocks -- a resident grid taking every
+// gridDim.x-th unit -- measured 3-30 % slower for any grid size: the
+// one-block-per-unit launch keeps the most rays in flight.)
+__host__ __device__ __forceinline__ int trace_vblocks(int tiles)
+{
+        return (tiles * (4 / VRT_RENDER_WAVES) + 7) & ~7;
+}
+
+// XCD-aware 8x8-pixel tile of block b of nb (a multiple of 8: the k_render
+// mapping) and this lane's pixel / sample.  u = the work unit.  Returns
+// false for padding blocks.
+__device__ __forceinline__ bool tile_lane(const RenderParams &p, int b, int nb, int &u, int &k, int &px, int &py,
                                           int &s, int &lx, int &ly)
 {
         constexpr int kQ = 4 / VRT_RENDER_WAVES;  // work units per tile
-        const int nb = gridDim.x, b = blockIdx.x;
-        const int per = (nb + 7) >> 3;
-        const int u = ((nb & 7) != 0) ? b : (b & 7) * per + (b >> 3);
+        u = (b & 7) * (nb >> 3) + (b >> 3);
         if (u >= p.tiles_this_rank * kQ)
                 return false;
         k = u / kQ;
@@ -2347,12 +2359,11 @@ __device__ __forceinline__ bool tile_lane(const RenderParams &p, int &k, int &px
 }
 
 template <bool kR64>
-__global__ __launch_bounds__(kRenderBlock) void k_light(LightParams p)
+__device__ __forceinline__ void light_unit(const LightParams &p, uint2 *stk, int b, int nb)
 {
-        __shared__ uint2 stk[kStack * kRenderBlock];
         const int tid = threadIdx.x;
-        int k, px, py, s, lx, ly;
-        if (!tile_lane(p.r, k, px, py, s, lx, ly))
+        int u, k, px, py, s, lx, ly;
+        if (!tile_lane(p.r, b, nb, u, k, px, py, s, lx, ly))
                 return;
         const CamParams &c = p.r.cam;
         const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
@@ -2378,6 +2389,13 @@ __global__ __launch_bounds__(kRenderBlock) void k_light(LightParams p)
         float *o = p.samp + 6 * key;
         o[0] = il.x; o[1] = il.y; o[2] = il.z;
         o[3] = nrm.x; o[4] = nrm.y; o[5] = nrm.z;
+}
+
+template <bool kR64>
+__global__ __launch_bounds__(kRenderBlock, VRT_TRACE_WAVES_PER_EU) void k_light(LightParams p)
+{
+        __shared__ uint2 stk[kStack * kRenderBlock];
+        light_unit<kR64>(p, stk, blockIdx.x, gridDim.x);
 }
 
 // Permute the per-sample records into the sorted (leaf, canonical) order so
@@ -2624,13 +2642,162 @@ __device__ __forceinline__ f3 cone_march_fast(const TraceParams &p, f3 o, f3 d)
         return diffuse;
 }
 
+#ifndef VRT_CONE_V
+#define VRT_CONE_V 4  // 1: cone_march_fast only; 2, 3: cone_march_axes without the cell / without the held il (A/B)
+#endif
+
+__device__ __forceinline__ int octant_of(const f3 &pt, const float4 &c)
+{
+        return (pt.x > c.x ? 4 : 0) + (pt.y > c.y ? 2 : 0) + (pt.z > c.z ? 1 : 0);
+}
+
+// cone_march_fast with one memory round trip per descent level and one per
+// light-map read (finite light map, every lane's cone having at most one
+// non-zero coefficient per axis: the caller checks).  The descent consumes
+// each 16-B (centre, child) record in the iteration that loads it (the next
+// octant is computed right away, also for a leaf, where it is unused), so
+// the record is one load; the root record is loaded once per cone.  A
+// light-map read fetches the coverage and, per axis, the illum vector of the
+// direction the cone faces (index a if co[a] != 0, else a + 3) together,
+// whatever the coverage; the sum over the 6 directions then runs in index
+// order 0..5 with the unselected slots adding +0: the terms cone_march_fast
+// skips (coefficient +0) and these +0 slots leave il unchanged, since il
+// starts at +0 and under round-to-nearest never becomes -0, so the sums are
+// bit-identical.
+//
+// kCell: the descent also records the cell of the point it followed -- per
+// axis the half-open interval (lo, hi] cut by the centres whose octant
+// choice it used (pt > centre: lo, else hi; the octree's cells are nested,
+// max/min keep the tightest) -- and the next step at the same split level
+// whose point lies in that cell makes the same choices at every node of the
+// path, so it reuses the node (and whether the descent ended above the split
+// level) without descending.  Any other step descends from the root.
+template <int kCell>
+__device__ __forceinline__ f3 cone_march_axes(const TraceParams &p, f3 o, f3 d, const float co[6])
+{
+        const float aperture = 0.577350269f, step = .1f, decay = 1.f;
+        const int jx = co[0] != 0.f ? 0 : 3, jy = co[1] != 0.f ? 1 : 4, jz = co[2] != 0.f ? 2 : 5;
+        const float cx = co[jx], cy = co[jy], cz = co[jz];
+        const float4 c0 = p.cc[0];
+        const uint32_t a0 = __float_as_uint(c0.w);
+        float dist = p.mindist;
+        float opacity = 0.f;
+        f3 diffuse = mk3(0.f, 0.f, 0.f);
+        int level = -1;
+        float bound = 0.f;
+        // the last descent's cell (kCell)
+        f3 lo = mk3(0.f, 0.f, 0.f), hi = lo;
+        int c_level = -1, c_split = 0;
+        uint32_t c_ni = 0;
+        float cov = 0.f;
+        f3 il = mk3(0.f, 0.f, 0.f);
+        for (int guard = 0; dist < p.maxdist && opacity < 1.f && guard < (1 << 16); ++guard) {
+                const f3 pt = o + d * dist;
+                const float diam = std_max(p.mindist, aperture * 2.f * dist);
+                if (p.maxdist < diam)
+                        break;
+                if (level < 0) {
+                        level = min(split_level_of(p.maxdist / diam, p.split_up), 63);
+                        bound = p.split_bound[level];
+                }
+                while (level > 0 && diam > bound) {
+                        --level;
+                        bound = p.split_bound[level];
+                }
+                int split = level;
+                uint32_t ni = 0;
+                bool same = false;
+                if (kCell && level == c_level && pt.x > lo.x && pt.x <= hi.x && pt.y > lo.y && pt.y <= hi.y &&
+                    pt.z > lo.z && pt.z <= hi.z) {
+                        split = c_split;
+                        ni = c_ni;
+                        same = kCell >= 2;
+                } else {
+                        uint32_t a = a0;
+                        float4 c = c0;
+                        int i = octant_of(pt, c0);
+                        if (kCell) {
+                                lo = mk3(-__builtin_inff(), -__builtin_inff(), -__builtin_inff());
+                                hi = mk3(__builtin_inff(), __builtin_inff(), __builtin_inff());
+                        }
+                        while (!(a & kLeafBit) && split) {
+                                if (kCell) {
+                                        if (i & 4) lo.x = std::max(lo.x, c.x); else hi.x = std::min(hi.x, c.x);
+                                        if (i & 2) lo.y = std::max(lo.y, c.y); else hi.y = std::min(hi.y, c.y);
+                                        if (i & 1) lo.z = std::max(lo.z, c.z); else hi.z = std::min(hi.z, c.z);
+                                }
+                                ni = a + (uint32_t)i;
+                                c = p.cc[ni];
+                                a = __float_as_uint(c.w);
+                                i = octant_of(pt, c);
+                                split--;
+                        }
+                        if (kCell) {
+                                c_level = level;
+                                c_split = split;
+                                c_ni = ni;
+                        }
+                }
+                if (split == 0) {
+                        if (!same) {  // (kCell 2: the same node's cov and il are still held)
+                                const LMRec *R = p.lm + ni;
+                                float L[9];
+                                cov = R->cov;
+#pragma unroll
+                                for (int k = 0; k < 3; ++k) {
+                                        L[k] = R->illum[3 * jx + k];
+                                        L[3 + k] = R->illum[3 * jy + k];
+                                        L[6 + k] = R->illum[3 * jz + k];
+                                }
+                                // the 10 loads issue together (not sunk into the branch)
+                                asm volatile("" : "+v"(cov), "+v"(L[0]), "+v"(L[1]), "+v"(L[2]), "+v"(L[3]),
+                                             "+v"(L[4]), "+v"(L[5]), "+v"(L[6]), "+v"(L[7]), "+v"(L[8]));
+                                if (cov != 0.f) {
+                                        const f3 tx = mk3(cx * L[0], cx * L[1], cx * L[2]);
+                                        const f3 ty = mk3(cy * L[3], cy * L[4], cy * L[5]);
+                                        const f3 tz = mk3(cz * L[6], cz * L[7], cz * L[8]);
+                                        const f3 z0 = mk3(0.f, 0.f, 0.f);
+                                        il = z0;
+                                        il = il + (jx == 0 ? tx : z0);
+                                        il = il + (jy == 1 ? ty : z0);
+                                        il = il + (jz == 2 ? tz : z0);
+                                        il = il + (jx == 3 ? tx : z0);
+                                        il = il + (jy == 4 ? ty : z0);
+                                        il = il + (jz == 5 ? tz : z0);
+                                }
+                        }
+                        if (cov != 0.f) {
+                                const float transparency = clampf(1.f - opacity, 0.f, 1.f);
+                                const float aa = cov * step;
+                                const float w = (1.f / (1.f + decay * dist)) * transparency * cov;
+                                diffuse = mk3(diffuse.x + w * il.x, diffuse.y + w * il.y, diffuse.z + w * il.z);
+                                opacity += transparency * aa;
+                        }
+                }
+                dist += step * diam;
+        }
+        return diffuse;
+}
+
 // cone_trace(root, cone, min_voxel_size) (VRT/voxel_octree.cc:276-311)
 __device__ __forceinline__ f3 cone_march_ref(const TraceParams &p, f3 o, f3 d);
 
 __device__ __forceinline__ f3 cone_march(const TraceParams &p, f3 o, f3 d)
 {
-        if (*p.lm_bad == 0u)
+        if (*p.lm_bad == 0u) {
+#if VRT_CONE_V >= 2
+                const f3 nd = -d;
+                float co[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i)
+                        co[i] = clampf(dot(illum_dir(i), nd), 0.f, 1.f);
+                const bool twin = (co[0] != 0.f && co[3] != 0.f) || (co[1] != 0.f && co[4] != 0.f) ||
+                                  (co[2] != 0.f && co[5] != 0.f);
+                if (!twin)
+                        return cone_march_axes<VRT_CONE_V - 2>(p, o, d, co);
+#endif
                 return cone_march_fast(p, o, d);
+        }
         return cone_march_ref(p, o, d);
 }
 
@@ -2713,8 +2880,8 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
         const int tid = threadIdx.x, lane = tid & 63;
-        int k, px, py, s, lx, ly;
-        if (!tile_lane(p.r, k, px, py, s, lx, ly))
+        int u, k, px, py, s, lx, ly;
+        if (!tile_lane(p.r, blockIdx.x, gridDim.x, u, k, px, py, s, lx, ly))
                 return;
         const CamParams &c = p.r.cam;
         const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
@@ -2767,17 +2934,12 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
 // Primary pass: trace()'s ray_march + get_albedo + leaf compute_illum(-d);
 // slot = work unit * kRenderBlock + tid.
 template <bool kR64>
-__global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
+__device__ __forceinline__ void trace_prim_unit(const TraceParams &p, uint2 *stk, int b, int nb)
 {
-        __shared__ uint2 stk[kStack * kRenderBlock];
         const int tid = threadIdx.x;
-        int k, px, py, s, lx, ly;
-        if (!tile_lane(p.r, k, px, py, s, lx, ly))
+        int u, k, px, py, s, lx, ly;
+        if (!tile_lane(p.r, b, nb, u, k, px, py, s, lx, ly))
                 return;
-        constexpr int kQ = 4 / VRT_RENDER_WAVES;
-        const int nb = gridDim.x, b = blockIdx.x;
-        const int u = ((nb & 7) != 0) ? b : (b & 7) * ((nb + 7) >> 3) + (b >> 3);
-        (void)kQ;
         const int64_t slot = (int64_t)u * kRenderBlock + tid;
         const CamParams &c = p.r.cam;
         const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
@@ -2802,6 +2964,13 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
         }
 }
 
+template <bool kR64>
+__global__ __launch_bounds__(kRenderBlock, VRT_TRACE_WAVES_PER_EU) void k_trace_prim(TraceParams p)
+{
+        __shared__ uint2 stk[kStack * kRenderBlock];
+        trace_prim_unit<kR64>(p, stk, blockIdx.x, gridDim.x);
+}
+
 // Cones + film: one wave per work unit of the primary pass (its 64 sample
 // slots: 16 pixels x 4 samples, lane = 4 * pixel + sample).  A hit lane
 // marches the 6 cones one after the other (the wave marches the same cone of
@@ -2812,7 +2981,10 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
 // with cross-lane reads (Film::add(c * .25f), VRT/main.cc:121) and the
 // pixel is written once: each sample record is read once, and no per-cone
 // result goes through memory.
-__global__ __launch_bounds__(64) void k_cones_film(TraceParams p)
+#ifndef VRT_CONES_WAVES_PER_EU
+#define VRT_CONES_WAVES_PER_EU 8  // 64 VGPRs; the spills are per cone, outside the step loop
+#endif
+__global__ __launch_bounds__(64, VRT_CONES_WAVES_PER_EU) void k_cones_film(TraceParams p)
 {
         const int u = blockIdx.x;
         constexpr int kQ = 4 / VRT_RENDER_WAVES;
@@ -2877,7 +3049,7 @@ hipError_t launch_light(const LightParams &p, hipStream_t st)
 {
         if (p.r.tiles_this_rank <= 0)
                 return hipSuccess;
-        const int grid = (p.r.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
+        const int grid = trace_vblocks(p.r.tiles_this_rank);
         hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_light<true> : k_light<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
         return hipGetLastError();
 }
@@ -2928,7 +3100,8 @@ hipError_t launch_trace(const TraceParams &p, hipStream_t st)
                 return hipGetLastError();
         }
         const int64_t nslots = (int64_t)p.r.tiles_this_rank * 256;
-        hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace_prim<true> : k_trace_prim<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
+        hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace_prim<true> : k_trace_prim<false>, dim3(grid), dim3(kRenderBlock),
+                           0, st, p);
         hipLaunchKernelGGL(k_cones_film, dim3((unsigned)(nslots / 64)), dim3(64), 0, st, p);
         return hipGetLastError();
 }
