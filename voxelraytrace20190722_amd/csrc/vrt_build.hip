@@ -455,7 +455,7 @@ hipError_t build_tree_device(int device, const float *pos, int ntri, const float
 // `bits` key bits, for the light-map accumulation (vrt_kernels.hip: leaf
 // key, canonical sample index); the same hipCUB / rocPRIM onesweep sort the
 // build's frontier uses, so hipCUB's templates compile in this one file.
-hipError_t sort_pairs_u32(void *temp, size_t *temp_bytes, const uint32_t *keys_in, uint32_t *keys_out,
+hipError_t sort_pairs_u64(void *temp, size_t *temp_bytes, const uint64_t *keys_in, uint64_t *keys_out,
                           const uint32_t *vals_in, uint32_t *vals_out, int64_t n, int bits, hipStream_t st)
 {
         return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out,

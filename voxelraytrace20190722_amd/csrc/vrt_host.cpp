@@ -1773,30 +1773,31 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
                 return rc;
         HIPCHK(hipMemsetAsync(s->d_lm, 0, (size_t)nnodes * sizeof(LMRec), s->stream));
         HIPCHK(hipMemsetAsync(d_bad, 0, 4, s->stream));
-        // scratch: keys/vals in+out, per-sample (illum, normal), sort temp
+        // scratch (sized for every sample hitting): 64-bit keys and 32-bit
+        // slots in + out, the per-hit (illum, normal) records and their copy
+        // in sorted order, the sort's temp
         size_t sort_bytes = 0;
-        const uint32_t miss_key = (uint32_t)nnodes;
-        int bits = 1;
-        while (bits < 32 && (miss_key >> bits) != 0)
-                ++bits;
-        HIPCHK(sort_pairs_u32(nullptr, &sort_bytes, nullptr, nullptr, nullptr, nullptr, ns, bits, s->stream));
-        // samp holds the per-sample records and, right after them, their
-        // copy gathered into sorted order (launch_lm_accum)
-        const size_t b4 = align_up((size_t)ns * 4), b24 = align_up((size_t)ns * 48);
+        int kbits = 1, lbits = 1;
+        while (kbits < 40 && (ns - 1) >> kbits)
+                ++kbits;
+        while (lbits < 32 && ((uint64_t)nnodes >> lbits) != 0)
+                ++lbits;
+        HIPCHK(sort_pairs_u64(nullptr, &sort_bytes, nullptr, nullptr, nullptr, nullptr, ns, kbits + lbits, s->stream));
+        const size_t b4 = align_up((size_t)ns * 4), b8 = align_up((size_t)ns * 8), b24 = align_up((size_t)ns * 48);
         const int64_t max_seg = std::max<int64_t>(1, s->info.nonempty_leaves);
         const size_t bseg = align_up((size_t)max_seg * 4);
         const size_t bend = align_up((size_t)nnodes * 4);
-        const size_t need = 4 * b4 + b24 + align_up(sort_bytes) + 256 + bseg + bend;
+        const size_t need = 2 * b8 + 2 * b4 + b24 + align_up(sort_bytes) + 256 + bseg + bend;
         HIPCHK(ensure_light_scratch(s, need));
         char *base = static_cast<char *>(s->d_light);
-        uint32_t *k_in = reinterpret_cast<uint32_t *>(base);
-        uint32_t *k_out = reinterpret_cast<uint32_t *>(base + b4);
-        uint32_t *v_in = reinterpret_cast<uint32_t *>(base + 2 * b4);
-        uint32_t *v_out = reinterpret_cast<uint32_t *>(base + 3 * b4);
-        float *samp = reinterpret_cast<float *>(base + 4 * b4);
-        void *temp = base + 4 * b4 + b24;
-        char *tail = base + 4 * b4 + b24 + align_up(sort_bytes);
-        unsigned long long *d_hits = reinterpret_cast<unsigned long long *>(tail);
+        uint64_t *k_in = reinterpret_cast<uint64_t *>(base);
+        uint64_t *k_out = reinterpret_cast<uint64_t *>(base + b8);
+        uint32_t *v_in = reinterpret_cast<uint32_t *>(base + 2 * b8);
+        uint32_t *v_out = reinterpret_cast<uint32_t *>(base + 2 * b8 + b4);
+        float *samp = reinterpret_cast<float *>(base + 2 * b8 + 2 * b4);
+        void *temp = base + 2 * b8 + 2 * b4 + b24;
+        char *tail = base + 2 * b8 + 2 * b4 + b24 + align_up(sort_bytes);
+        unsigned int *d_count = reinterpret_cast<unsigned int *>(tail);
         unsigned int *d_nseg = reinterpret_cast<unsigned int *>(tail + 64);
         uint32_t *d_seg = reinterpret_cast<uint32_t *>(tail + 256);
         uint32_t *d_seg_end = reinterpret_cast<uint32_t *>(tail + 256 + bseg);
@@ -1806,15 +1807,20 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         fill_render_params(s, light_cam, light_film, 0, 1, &lp.r);
         lp.ptx = ptx;
         lp.pty = pty;
-        lp.miss_key = miss_key;
+        lp.kbits = kbits;
+        lp.count = d_count;
         lp.keys = k_in;
+        lp.vals = v_in;
         lp.samp = samp;
-        lp.hits = d_hits;
         HIPCHK(hipEventRecord(s->ev0, s->stream));
         HIPCHK(launch_light(lp, s->stream));
-        HIPCHK(launch_iota(v_in, ns, s->stream));
-        HIPCHK(sort_pairs_u32(temp, &sort_bytes, k_in, k_out, v_in, v_out, ns, bits, s->stream));
-        HIPCHK(launch_lm_accum(ns, k_out, v_out, samp, miss_key, d_seg, d_nseg, max_seg, d_seg_end, s->d_lm,
+        // the sort takes its length on the host: the one mid-build sync
+        unsigned int nhit = 0;
+        HIPCHK(hipMemcpyAsync(&nhit, d_count, sizeof nhit, hipMemcpyDeviceToHost, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        if (nhit > 0)
+                HIPCHK(sort_pairs_u64(temp, &sort_bytes, k_in, k_out, v_in, v_out, nhit, kbits + lbits, s->stream));
+        HIPCHK(launch_lm_accum(nhit, k_out, v_out, kbits, samp, d_seg, d_nseg, max_seg, d_seg_end, s->d_lm,
                                s->stream));
         // cone_trace_init_filter: leaves, then internal levels bottom-up
         HIPCHK(launch_lm_leaves(s->dev.nodes, nnodes, s->d_lm, s->stream));
@@ -1824,13 +1830,11 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         HIPCHK(launch_lm_aux(s->dev.nodes, s->d_lm, nnodes, d_cc, d_bad, s->stream));
         HIPCHK(hipEventRecord(s->ev1, s->stream));
         s->timed = true;
-        unsigned long long h = 0;
-        HIPCHK(hipMemcpyAsync(&h, d_hits, sizeof h, hipMemcpyDeviceToHost, s->stream));
         if (int rc = scratch_release(s, s->stream))
                 return rc;
         HIPCHK(hipStreamSynchronize(s->stream));
         if (hits)
-                *hits = (int64_t)h;
+                *hits = (int64_t)nhit;
         s->lm_ready = true;
         return VRT_OK;
 }

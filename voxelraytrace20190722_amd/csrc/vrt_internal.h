@@ -378,15 +378,19 @@ static_assert(sizeof(LMRec) == 80, "LMRec must be 80 B");
 
 // Light pass (VRT/main.cc:79-97) over r's film: every sample of the
 // canonical single-threaded order k (render_mt task t = tx*8+ty of
-// ptx x pty pixels, row-major, samples 0..3) writes keys[k] = hit leaf node
-// (~0u on a miss) and samp[6k..6k+5] = get_diffuse rgb, isect normal.
+// ptx x pty pixels, row-major, samples 0..3) that hits takes the next slot
+// j of a compact list (one atomic add per wave) and writes keys[j] = hit leaf
+// << kbits | k, vals[j] = j and samp[6j..6j+5] = get_diffuse rgb, isect
+// normal; *count ends as the number of hits.  Sorting the pairs by key puts
+// each leaf's samples together in canonical order.
 struct LightParams {
         RenderParams r;
         int32_t ptx, pty;
-        uint32_t miss_key;   // key of a miss (= node count: sorts last)
-        uint32_t *keys;
+        int32_t kbits;       // bits of the canonical index k
+        unsigned int *count;
+        uint64_t *keys;
+        uint32_t *vals;
         float *samp;
-        unsigned long long *hits;  // += hit samples
 };
 
 // Cone-tracing render (trace(), VRT/main.cc:10-30 + cone_trace,
@@ -463,8 +467,8 @@ hipError_t launch_light(const LightParams &p, hipStream_t st);
 // samp: n x 6 floats followed by room for their sorted copy (n x 6);
 // seg_start: max_seg entries (>= non-empty leaves), nseg zeroed; seg_end:
 // one entry per node (each hit leaf's run end is written)
-hipError_t launch_lm_accum(int64_t n, const uint32_t *keys_sorted, const uint32_t *vals_sorted,
-                           const float *samp, uint32_t miss_key, uint32_t *seg_start, unsigned int *nseg,
+hipError_t launch_lm_accum(int64_t n, const uint64_t *keys_sorted, const uint32_t *vals_sorted, int kbits,
+                           const float *samp, uint32_t *seg_start, unsigned int *nseg,
                            int64_t max_seg, uint32_t *seg_end, LMRec *lm, hipStream_t st);
 hipError_t launch_lm_leaves(const NodeRec *nodes, int64_t nnodes, LMRec *lm, hipStream_t st);
 hipError_t launch_lm_level(const NodeRec *nodes, int64_t begin, int64_t end, LMRec *lm, hipStream_t st);
@@ -474,9 +478,8 @@ hipError_t launch_lm_aux(const NodeRec *nodes, const LMRec *lm, int64_t n, float
                          hipStream_t st);
 // stable radix sort of (key, value) pairs on the low `bits` key bits
 // (vrt_build.hip); temp == nullptr queries *temp_bytes
-hipError_t sort_pairs_u32(void *temp, size_t *temp_bytes, const uint32_t *keys_in, uint32_t *keys_out,
+hipError_t sort_pairs_u64(void *temp, size_t *temp_bytes, const uint64_t *keys_in, uint64_t *keys_out,
                           const uint32_t *vals_in, uint32_t *vals_out, int64_t n, int bits, hipStream_t st);
-hipError_t launch_iota(uint32_t *v, int64_t n, hipStream_t st);
 hipError_t launch_rgbe(const float *img, int64_t npx, int comp, uint8_t *out, hipStream_t st);
 hipError_t launch_selftest_order(const float *dist, const uint32_t *hm, int64_t n, uint32_t *out,
                                  const float *depth, const int32_t *len, int64_t m, int32_t stride,

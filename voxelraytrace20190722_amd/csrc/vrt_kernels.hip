@@ -2322,27 +2322,30 @@ __device__ __forceinline__ f3 illum_dir(int i)
         return mk3(ax == 0 ? v : 0.f, ax == 1 ? v : 0.f, ax == 2 ? v : 0.f);
 }
 
-#ifndef VRT_TRACE_WAVES_PER_EU
-#define VRT_TRACE_WAVES_PER_EU 1
-#endif
-
 // Grid of the light / trace passes: one one-wave block per work unit,
-// rounded up to 8 blocks.  (Looping blocks -- a resident grid taking every
-// gridDim.x-th unit -- measured 3-30 % slower for any grid size: the
-// one-block-per-unit launch keeps the most rays in flight.)
+// rounded up to 8 blocks.  Measured against it and slower: looping blocks
+// (a resident grid taking every gridDim.x-th unit, 3-30 % slower for any grid
+// size) and blocks of 2 / 4 / 8 consecutive units (light pass -10 / -25 /
+// -43 %): the one-block-per-unit launch keeps the most rays in flight.
 __host__ __device__ __forceinline__ int trace_vblocks(int tiles)
 {
         return (tiles * (4 / VRT_RENDER_WAVES) + 7) & ~7;
 }
 
-// XCD-aware 8x8-pixel tile of block b of nb (a multiple of 8: the k_render
-// mapping) and this lane's pixel / sample.  u = the work unit.  Returns
-// false for padding blocks.
-__device__ __forceinline__ bool tile_lane(const RenderParams &p, int b, int nb, int &u, int &k, int &px, int &py,
+// XCD-aware block order: block b of nb (a multiple of 8) -> its place in
+// the launch's work (blocks b, b + 8, ... run on one XCD and take
+// consecutive places: the k_render mapping)
+__device__ __forceinline__ int xcd_place(int b, int nb)
+{
+        return (b & 7) * (nb >> 3) + (b >> 3);
+}
+
+// 8x8-pixel tile of work unit u and this lane's pixel / sample.  Returns
+// false for padding units.
+__device__ __forceinline__ bool tile_lane(const RenderParams &p, int u, int &k, int &px, int &py,
                                           int &s, int &lx, int &ly)
 {
         constexpr int kQ = 4 / VRT_RENDER_WAVES;  // work units per tile
-        u = (b & 7) * (nb >> 3) + (b >> 3);
         if (u >= p.tiles_this_rank * kQ)
                 return false;
         k = u / kQ;
@@ -2359,11 +2362,11 @@ __device__ __forceinline__ bool tile_lane(const RenderParams &p, int b, int nb, 
 }
 
 template <bool kR64>
-__device__ __forceinline__ void light_unit(const LightParams &p, uint2 *stk, int b, int nb)
+__device__ __forceinline__ void light_unit(const LightParams &p, uint2 *stk, int u)
 {
         const int tid = threadIdx.x;
-        int u, k, px, py, s, lx, ly;
-        if (!tile_lane(p.r, b, nb, u, k, px, py, s, lx, ly))
+        int k, px, py, s, lx, ly;
+        if (!tile_lane(p.r, u, k, px, py, s, lx, ly))
                 return;
         const CamParams &c = p.r.cam;
         const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
@@ -2372,30 +2375,27 @@ __device__ __forceinline__ void light_unit(const LightParams &p, uint2 *stk, int
                                  dn, c.tmin, c.tmax);
         MarchResult m;
         ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
+        if (!m.hit)
+                return;
         // canonical order: render_mt task t = tx*8 + ty (VRT/camera.h:50-56)
         const int tx = px / p.ptx, ty = py / p.pty;
         const int64_t task = (int64_t)tx * 8 + ty;
         const int64_t key = ((task * p.pty + (py - ty * p.pty)) * p.ptx + (px - tx * p.ptx)) * 4 + s;
-        const unsigned long long wave_hits = __popcll(__ballot(m.hit));
-        if ((tid & 63) == 0 && wave_hits)
-                atomicAdd(p.hits, wave_hits);
-        if (!m.hit) {
-                p.keys[key] = p.miss_key;
-                return;
-        }
         f3 nrm;
         const f3 il = shade_hit(p.r.sc, r, m, nrm);
-        p.keys[key] = m.node;
-        float *o = p.samp + 6 * key;
+        const uint32_t j = atomicAdd(p.count, 1u);  // the hit lanes' adds: one atomic per wave
+        p.keys[j] = ((uint64_t)m.node << p.kbits) | (uint64_t)key;
+        p.vals[j] = j;
+        float *o = p.samp + 6 * (int64_t)j;
         o[0] = il.x; o[1] = il.y; o[2] = il.z;
         o[3] = nrm.x; o[4] = nrm.y; o[5] = nrm.z;
 }
 
 template <bool kR64>
-__global__ __launch_bounds__(kRenderBlock, VRT_TRACE_WAVES_PER_EU) void k_light(LightParams p)
+__global__ __launch_bounds__(kRenderBlock) void k_light(LightParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
-        light_unit<kR64>(p, stk, blockIdx.x, gridDim.x);
+        light_unit<kR64>(p, stk, xcd_place(blockIdx.x, gridDim.x));
 }
 
 // Permute the per-sample records into the sorted (leaf, canonical) order so
@@ -2413,21 +2413,19 @@ __global__ __launch_bounds__(256) void k_lm_gather(int64_t n, const uint32_t *__
         o[2] = q[2];
 }
 
-// Start index of every run of equal (hit) leaf keys (run order is
-// irrelevant) and, per leaf, the end of its run.
-__global__ __launch_bounds__(256) void k_lm_segments(int64_t n, const uint32_t *__restrict__ keys,
-                                                     uint32_t miss_key, uint32_t *__restrict__ seg_start,
-                                                     unsigned int *__restrict__ nseg, uint32_t *__restrict__ seg_end)
+// Start index of every run of equal leaf keys (run order is irrelevant)
+// and, per leaf, the end of its run.
+__global__ __launch_bounds__(256) void k_lm_segments(int64_t n, const uint64_t *__restrict__ keys, int kbits,
+                                                     uint32_t *__restrict__ seg_start, unsigned int *__restrict__ nseg,
+                                                     uint32_t *__restrict__ seg_end)
 {
         const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
         if (i >= n)
                 return;
-        const uint32_t leaf = keys[i];
-        if (leaf >= miss_key)
-                return;
-        if (i + 1 == n || keys[i + 1] != leaf)
+        const uint64_t leaf = keys[i] >> kbits;
+        if (i + 1 == n || (keys[i + 1] >> kbits) != leaf)
                 seg_end[leaf] = (uint32_t)(i + 1);
-        if (i > 0 && keys[i - 1] == leaf)
+        if (i > 0 && (keys[i - 1] >> kbits) == leaf)
                 return;
         seg_start[atomicAdd(nseg, 1u)] = (uint32_t)i;
 }
@@ -2441,7 +2439,7 @@ __global__ __launch_bounds__(256) void k_lm_segments(int64_t n, const uint32_t *
 // time ahead of the chain of adds instead of one load round trip per add.
 constexpr int kLmBatch = 8;
 __global__ __launch_bounds__(256) void k_lm_accum(const float *__restrict__ samp,
-                                                  const uint32_t *__restrict__ keys,
+                                                  const uint64_t *__restrict__ keys, int kbits,
                                                   const uint32_t *__restrict__ seg_start,
                                                   const unsigned int *__restrict__ nseg,
                                                   const uint32_t *__restrict__ seg_end, LMRec *__restrict__ lm)
@@ -2452,7 +2450,7 @@ __global__ __launch_bounds__(256) void k_lm_accum(const float *__restrict__ samp
                 return;
         const int d = l / 3, c = l % 3;
         const int64_t i0 = seg_start[seg];
-        const uint32_t leaf = keys[i0];
+        const uint32_t leaf = (uint32_t)(keys[i0] >> kbits);
         const int64_t i1 = seg_end[leaf];
         const f3 dir = illum_dir(d);
         float acc = 0.f;
@@ -2880,8 +2878,9 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
         const int tid = threadIdx.x, lane = tid & 63;
-        int u, k, px, py, s, lx, ly;
-        if (!tile_lane(p.r, blockIdx.x, gridDim.x, u, k, px, py, s, lx, ly))
+        const int u = xcd_place(blockIdx.x, gridDim.x);
+        int k, px, py, s, lx, ly;
+        if (!tile_lane(p.r, u, k, px, py, s, lx, ly))
                 return;
         const CamParams &c = p.r.cam;
         const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
@@ -2934,11 +2933,11 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
 // Primary pass: trace()'s ray_march + get_albedo + leaf compute_illum(-d);
 // slot = work unit * kRenderBlock + tid.
 template <bool kR64>
-__device__ __forceinline__ void trace_prim_unit(const TraceParams &p, uint2 *stk, int b, int nb)
+__device__ __forceinline__ void trace_prim_unit(const TraceParams &p, uint2 *stk, int u)
 {
         const int tid = threadIdx.x;
-        int u, k, px, py, s, lx, ly;
-        if (!tile_lane(p.r, b, nb, u, k, px, py, s, lx, ly))
+        int k, px, py, s, lx, ly;
+        if (!tile_lane(p.r, u, k, px, py, s, lx, ly))
                 return;
         const int64_t slot = (int64_t)u * kRenderBlock + tid;
         const CamParams &c = p.r.cam;
@@ -2965,10 +2964,10 @@ __device__ __forceinline__ void trace_prim_unit(const TraceParams &p, uint2 *stk
 }
 
 template <bool kR64>
-__global__ __launch_bounds__(kRenderBlock, VRT_TRACE_WAVES_PER_EU) void k_trace_prim(TraceParams p)
+__global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
-        trace_prim_unit<kR64>(p, stk, blockIdx.x, gridDim.x);
+        trace_prim_unit<kR64>(p, stk, xcd_place(blockIdx.x, gridDim.x));
 }
 
 // Cones + film: one wave per work unit of the primary pass (its 64 sample
@@ -3038,13 +3037,6 @@ __global__ __launch_bounds__(64, VRT_CONES_WAVES_PER_EU) void k_cones_film(Trace
         }
 }
 
-__global__ void k_iota(uint32_t *v, int64_t n)
-{
-        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        if (i < n)
-                v[i] = (uint32_t)i;
-}
-
 hipError_t launch_light(const LightParams &p, hipStream_t st)
 {
         if (p.r.tiles_this_rank <= 0)
@@ -3054,8 +3046,8 @@ hipError_t launch_light(const LightParams &p, hipStream_t st)
         return hipGetLastError();
 }
 
-hipError_t launch_lm_accum(int64_t n, const uint32_t *keys_sorted, const uint32_t *vals_sorted,
-                           const float *samp, uint32_t miss_key, uint32_t *seg_start, unsigned int *nseg,
+hipError_t launch_lm_accum(int64_t n, const uint64_t *keys_sorted, const uint32_t *vals_sorted, int kbits,
+                           const float *samp, uint32_t *seg_start, unsigned int *nseg,
                            int64_t max_seg, uint32_t *seg_end, LMRec *lm, hipStream_t st)
 {
         if (n <= 0)
@@ -3065,11 +3057,10 @@ hipError_t launch_lm_accum(int64_t n, const uint32_t *keys_sorted, const uint32_
         float *sorted = const_cast<float *>(samp) + 6 * n;
         const unsigned g = (unsigned)((n + 255) / 256);
         hipLaunchKernelGGL(k_lm_gather, dim3(g), dim3(256), 0, st, n, vals_sorted, samp, sorted);
-        hipLaunchKernelGGL(k_lm_segments, dim3(g), dim3(256), 0, st, n, keys_sorted, miss_key, seg_start, nseg,
-                           seg_end);
+        hipLaunchKernelGGL(k_lm_segments, dim3(g), dim3(256), 0, st, n, keys_sorted, kbits, seg_start, nseg, seg_end);
         if (max_seg > 0)
                 hipLaunchKernelGGL(k_lm_accum, dim3((unsigned)((max_seg + 7) / 8)), dim3(256), 0, st, sorted,
-                                   keys_sorted, seg_start, nseg, seg_end, lm);
+                                   keys_sorted, kbits, seg_start, nseg, seg_end, lm);
         return hipGetLastError();
 }
 
@@ -3094,14 +3085,14 @@ hipError_t launch_trace(const TraceParams &p, hipStream_t st)
 {
         if (p.r.tiles_this_rank <= 0)
                 return hipSuccess;
-        const int grid = (p.r.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
+        const int grid = trace_vblocks(p.r.tiles_this_rank);
         if (!p.rec) {
                 hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace<true> : k_trace<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
                 return hipGetLastError();
         }
         const int64_t nslots = (int64_t)p.r.tiles_this_rank * 256;
-        hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace_prim<true> : k_trace_prim<false>, dim3(grid), dim3(kRenderBlock),
-                           0, st, p);
+        hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace_prim<true> : k_trace_prim<false>,
+                           dim3(trace_vblocks(p.r.tiles_this_rank)), dim3(kRenderBlock), 0, st, p);
         hipLaunchKernelGGL(k_cones_film, dim3((unsigned)(nslots / 64)), dim3(64), 0, st, p);
         return hipGetLastError();
 }
@@ -3112,14 +3103,6 @@ hipError_t launch_lm_aux(const NodeRec *nodes, const LMRec *lm, int64_t n, float
         if (n <= 0)
                 return hipSuccess;
         hipLaunchKernelGGL(k_lm_aux, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nodes, lm, n, cc, bad);
-        return hipGetLastError();
-}
-
-hipError_t launch_iota(uint32_t *v, int64_t n, hipStream_t st)
-{
-        if (n <= 0)
-                return hipSuccess;
-        hipLaunchKernelGGL(k_iota, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, n);
         return hipGetLastError();
 }
 
