@@ -250,7 +250,16 @@ int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
  * failure after its first kernel is enqueued (the error path that must
  * leave the scene's work-queue slot usable by later launches). */
 #define VRT_TEST_FAIL_LAUNCH 2
+/* VRT_TEST_SPILL_ALL makes config-5's ray compaction stop a wave's rays as
+ * soon as one of them has ended (every resume round but the last likewise),
+ * so that nearly every secondary ray is saved and resumed at least once. */
+#define VRT_TEST_SPILL_ALL 4
 int vrt_set_test_flags(int flags);
+
+/* Diagnostic: the records appended to each compaction queue (phase A, then
+ * resume rounds 1..3) by the scene's last config-5 launch; waits for it.
+ * All 0 when that launch used no compaction. */
+int vrt_secondary_spill_counts(vrt_scene *s, int64_t counts[4]);
 
 /* The kernels' own travorder sort (std::sort of the 8 Items by dist,
  * VRT/voxel_octree.cc:77-97) and ray_march_isect min_element

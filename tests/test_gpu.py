@@ -364,6 +364,35 @@ def test_secondary_occlusion_walk_matches_ordered_walk(proxy_small, depth):
         assert 0 < d["hit"].sum() < d["hit"].size  # both outcomes occur
 
 
+@pytest.mark.parametrize("depth", [6, 8])
+@pytest.mark.parametrize("flags", [0, vrt.TEST_SPILL_ALL])
+def test_secondary_compaction_matches_oracle(proxy_small, depth, flags):
+    """Config-5 ray compaction: rays still walking when few
+    lanes of their wave are go to a queue with their walk state and are
+    resumed 64 to a wave.  Every ray's hit boolean and the visibility image
+    equal the oracle's; flags=TEST_SPILL_ALL stops every wave at its first
+    ended ray (and every resume round but the last), so nearly all rays are
+    saved and resumed mid-walk at least once."""
+    tree = vrt.VoxelOctree(proxy_small, depth)
+    osc = po.Scene(proxy_small, depth)
+    mn, mx = tree.root_box
+    fov, eye, spot, up = vrt.sweep_pose(mn, mx, 6, 16)
+    film = vrt.Film(1, 1, 96, 64)
+    vrt.set_test_flags(flags)
+    try:
+        vis, rays, d = tree.render_secondary(vrt.Camera(fov, eye, spot, up), film, spp=64, ids="hit")
+        counts = tree.secondary_spill_counts()
+    finally:
+        vrt.set_test_flags(0)
+    ovis, orays, od = osc.render_secondary(po.camera(fov, eye, spot, up), 1.0, 1.0, 96, 64, spp=64)
+    assert rays == orays
+    assert np.array_equal(d["hit"], od["hit"])
+    assert np.array_equal(bits(vis), bits(ovis))
+    assert counts[0] > 0, counts  # phase A stopped rays
+    if flags:  # most stopped rays are stopped again in round 1
+        assert counts[0] > rays // 20 and counts[1] > counts[0] // 2, (counts, rays)
+
+
 @pytest.mark.parametrize("nx,ny,nranks", [(72, 40, 3), (512, 40, 8)])
 def test_secondary_rank_partition_sums_to_image(proxy_small, nx, ny, nranks):
     """Each rank writes exactly the pixels of its 8x8 tiles (dist.py

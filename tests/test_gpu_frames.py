@@ -121,10 +121,12 @@ def test_c5_1080p_depth8_secondary_whole_frame(proxy):
     cam = vrt.Camera(fov, eye, spot, up)
     film = vrt.Film(1, 1, 1920, 1080)
     vis, rays = tree.render_secondary(cam, film, spp=64)
+    counts = tree.secondary_spill_counts()
     ovis, orays = osc.render_secondary(po.camera(fov, eye, spot, up), 1.0, 1.0, 1920, 1080, spp=64,
                                        nthreads=NTH, ids=False)
     assert rays == orays > 1920 * 1080 * 32
     assert np.array_equal(bits(vis), bits(ovis))
+    assert counts[0] > 0, counts  # the frame ran with its ray compaction
     prim = torch.zeros(1920 * 1080 * 8, dtype=torch.float32, device="cuda:0")
     dvis = torch.zeros((1080, 1920), dtype=torch.float32, device="cuda:0")
     tree.render_secondary_device(cam, film, 64, 0, 1, prim.data_ptr(), dvis.data_ptr(), None)

@@ -378,18 +378,24 @@ class VoxelOctree:
 
     def render_secondary(self, cam, film, spp=64, ids=False):
         """Config 5: per-pixel sky visibility from `spp` stochastic secondary
-        rays -> (ny, nx) float32 image, rays traced (+ per-ray id dict)."""
+        rays -> (ny, nx) float32 image, rays traced (+ per-ray id dict).
+        ids=True: per-ray hit, triangle and voxel ids (the ordered walk);
+        ids="hit": per-ray hit booleans only (the occlusion walk with its
+        compaction, as without ids)."""
         nx, ny = film.nx, film.ny
         vis = np.zeros((ny, nx), np.float32)
         rays = C.c_int64()
         d = None
         if ids:
             ns = nx * ny * spp
-            d = {"hit": np.zeros(ns, np.int32), "tri": np.zeros(ns, np.int32), "voxel": np.zeros(ns, np.uint32)}
+            d = {"hit": np.zeros(ns, np.int32)}
+            if ids != "hit":
+                d.update(tri=np.zeros(ns, np.int32), voxel=np.zeros(ns, np.uint32))
         check(lib().vrt_render_secondary(self.h, C.byref(cam.c), C.byref(film.c), int(spp), ptr(vis, _ffi.f32p),
                                          ptr(d["hit"], _ffi.i32p) if d else None,
-                                         ptr(d["tri"], _ffi.i32p) if d else None,
-                                         ptr(d["voxel"], _ffi.u32p) if d else None, C.byref(rays)),
+                                         ptr(d["tri"], _ffi.i32p) if d and "tri" in d else None,
+                                         ptr(d["voxel"], _ffi.u32p) if d and "voxel" in d else None,
+                                         C.byref(rays)),
               "vrt_render_secondary")
         return (vis, rays.value, d) if ids else (vis, rays.value)
 
@@ -409,6 +415,13 @@ class VoxelOctree:
         """Launch hint (vrt_scene_set_frames_in_flight): n >= 2 frames kept
         in flight on different streams -> half-chip persistent grids."""
         check(lib().vrt_scene_set_frames_in_flight(self.h, int(n)), "vrt_scene_set_frames_in_flight")
+
+    def secondary_spill_counts(self):
+        """Records appended to each config-5 compaction queue (phase A, resume
+        rounds 1..3) by the last secondary launch (vrt_secondary_spill_counts)."""
+        c = (C.c_int64 * 4)()
+        check(lib().vrt_secondary_spill_counts(self.h, c), "vrt_secondary_spill_counts")
+        return list(c)
 
     def last_kernel_ms(self):
         ms = C.c_float()
@@ -664,6 +677,7 @@ def build_id():
 
 TEST_FORCE_DEFER = 1  # include/vrt.h VRT_TEST_FORCE_DEFER
 TEST_FAIL_LAUNCH = 2  # include/vrt.h VRT_TEST_FAIL_LAUNCH
+TEST_SPILL_ALL = 4  # include/vrt.h VRT_TEST_SPILL_ALL
 
 
 def set_test_flags(flags):

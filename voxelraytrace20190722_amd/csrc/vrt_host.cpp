@@ -339,6 +339,11 @@ struct vrt_scene {
         size_t light_bytes = 0;
         void *d_trace = nullptr;  // split-trace scratch (records + colours)
         size_t trace_bytes = 0;
+        // config-5 ray compaction (SpillQueues): round counters + two record
+        // queues of spill_cap records each
+        void *d_spill = nullptr;
+        uint32_t spill_cap = 0;   // chunks per queue
+        bool spill_used = false;  // the last config-5 launch compacted (vrt_secondary_spill_counts)
         // device
         void *d_mem = nullptr;
         DevScene dev{};
@@ -989,7 +994,8 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
 {
         if (!s)
                 return;
-        if (s->d_mem || s->d_lm || s->d_light || s->d_trace || s->stream || s->ev0 || s->ev1 || s->scratch_ev) {
+        if (s->d_mem || s->d_lm || s->d_light || s->d_trace || s->d_spill || s->stream || s->ev0 || s->ev1 ||
+            s->scratch_ev) {
                 (void)hipSetDevice(s->device);
                 if (s->stream)
                         (void)hipStreamSynchronize(s->stream);
@@ -1001,6 +1007,8 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                         (void)hipFree(s->d_light);
                 if (s->d_trace)
                         (void)hipFree(s->d_trace);
+                if (s->d_spill)
+                        (void)hipFree(s->d_spill);
                 if (s->ev0)
                         (void)hipEventDestroy(s->ev0);
                 if (s->ev1)
@@ -1250,6 +1258,54 @@ static int render_launch(vrt_scene *s, RenderParams &p, bool instrumented, hipSt
         return VRT_OK;
 }
 
+static int scratch_acquire(vrt_scene *s, hipStream_t st);
+static int scratch_release(vrt_scene *s, hipStream_t st);
+
+// Compaction queues of one config-5 launch (SpillQueues): room
+// for every secondary ray of this rank, in chunks, up to kSpillCapMax records
+// per queue (a full queue only means the rays beyond it finish in their
+// first wave); the round counters zeroed on the stream.  The buffers are
+// scene scratch: the launch holds them through scratch_acquire /
+// scratch_release.  sq->nchunks stays 0 (no compaction) when the build
+// disables it or the allocation fails.
+constexpr uint32_t kSpillCapMax = 1u << 24;  // 2 GiB of records per queue
+static int spill_setup(vrt_scene *s, int64_t rays, hipStream_t st, SpillQueues *sq)
+{
+        *sq = spill_defaults();
+        if (sq->t_first == 0 || rays <= 0)
+                return VRT_OK;
+        // + one partly filled chunk per wave of a resident grid
+        const int64_t want = rays + (int64_t)std::max(1, s->dev.sec_blocks) * 4 * kSpillChunk;
+        const uint32_t nch = (uint32_t)((std::min<int64_t>(want, kSpillCapMax) + kSpillChunk - 1) / kSpillChunk);
+        const size_t ctr_bytes = (size_t)kSpillMaxRounds * kSpillCtrStride * 4;
+        const size_t fill_bytes = ((size_t)nch * 4 + 255) & ~(size_t)255;
+        if (s->spill_cap < nch) {
+                if (s->d_spill) {
+                        HIPCHK(hipDeviceSynchronize());  // earlier launches on any stream may use it
+                        (void)hipFree(s->d_spill);
+                        s->d_spill = nullptr;
+                        s->spill_cap = 0;
+                }
+                if (hipMalloc(&s->d_spill, ctr_bytes + 2 * fill_bytes + 2 * (size_t)nch * kSpillChunk * sizeof(SpillRec)) !=
+                    hipSuccess) {
+                        (void)hipGetLastError();
+                        s->d_spill = nullptr;
+                        return VRT_OK;  // no compaction
+                }
+                s->spill_cap = nch;
+        }
+        const size_t fb = ((size_t)s->spill_cap * 4 + 255) & ~(size_t)255;
+        char *b = static_cast<char *>(s->d_spill);
+        sq->ctr = reinterpret_cast<uint32_t *>(b);
+        sq->fill[0] = reinterpret_cast<uint32_t *>(b + ctr_bytes);
+        sq->fill[1] = reinterpret_cast<uint32_t *>(b + ctr_bytes + fb);
+        sq->rec[0] = reinterpret_cast<SpillRec *>(b + ctr_bytes + 2 * fb);
+        sq->rec[1] = sq->rec[0] + (size_t)s->spill_cap * kSpillChunk;
+        sq->nchunks = s->spill_cap;
+        HIPCHK(hipMemsetAsync(sq->ctr, 0, ctr_bytes, st));
+        return VRT_OK;
+}
+
 // One config-5 launch (k_primary1 + secondary rays) on stream st (caller
 // holds s->mu).
 static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int rank, int nranks, float *d_prim,
@@ -1259,12 +1315,26 @@ static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int ra
         WorkQueue q;
         std::memset(&q, 0, sizeof q);
         (void)hipGetLastError();  // a leftover error of an earlier call is not this launch's
-        if (secondary_uses_queue(p.sc))
+        SpillQueues sq;
+        std::memset(&sq, 0, sizeof sq);
+        if (secondary_uses_queue(p.sc)) {
                 if (int rc = queue_take(s, st, &q, &slot))
                         return rc;
+                if (!s_tri && !s_vox) {  // the occlusion walk: compaction
+                        const int64_t rays = deal_count(tile_deal(p.ntx, p.nty, nranks), rank) * 64 * (int64_t)spp;
+                        if (int rc = scratch_acquire(s, st))
+                                return rc;
+                        if (int rc = spill_setup(s, rays, st, &sq))
+                                return rc;
+                }
+        }
         int waves = 0, units[8];
+        s->spill_used = sq.nchunks > 0;
         const hipError_t e = launch_secondary(p, spp, rank, nranks, scene_res(s), d_prim, d_vis, s_hit, s_tri,
-                                              s_vox, slot >= 0 ? &q : nullptr, st, &waves, units);
+                                              s_vox, slot >= 0 ? &q : nullptr, st, &waves, units, &sq);
+        if (sq.nchunks > 0)
+                if (int rc = scratch_release(s, st))
+                        return rc;
         if (e != hipSuccess) {
                 if (slot >= 0)
                         queue_reset(s, slot, st);
@@ -1625,6 +1695,26 @@ extern "C" int vrt_render_secondary_device(vrt_scene *s, const vrt_camera *cam,
                 return rc;
         HIPCHK(hipEventRecord(s->ev1, st));
         s->timed = true;
+        return VRT_OK;
+}
+
+extern "C" int vrt_secondary_spill_counts(vrt_scene *s, int64_t counts[4])
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !counts)
+                return fail(VRT_E_INVALID, "null argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        for (int r = 0; r < 4; ++r)
+                counts[r] = 0;
+        if (!s->spill_used || !s->d_spill)
+                return VRT_OK;
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipDeviceSynchronize());
+        std::vector<uint32_t> c((size_t)kSpillMaxRounds * kSpillCtrStride);
+        HIPCHK(hipMemcpy(c.data(), s->d_spill, c.size() * 4, hipMemcpyDeviceToHost));
+        for (int r = 0; r < 4 && r < kSpillMaxRounds; ++r)
+                counts[r] = c[(size_t)r * kSpillCtrStride + 2];  // records (spill_close)
         return VRT_OK;
 }
 

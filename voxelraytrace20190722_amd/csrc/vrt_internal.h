@@ -209,6 +209,48 @@ __host__ __device__ inline int slice_unit(int units, int x, int u, int ch)
         return ((u / ch) * 8 + x) * ch + u % ch;
 }
 
+// Config-5 ray compaction (k_secondary_p + k_sec_resume).  A
+// wave walks one pixel's secondary rays until fewer than `t_first` of them
+// are still walking; it then stops, and each of those rays writes its walk
+// state -- the ray, the node it was about to visit next and its DFS stack --
+// to queue 0.  Resume round r (1..rounds) packs queue r-1's rays 64 to a
+// wave and continues their walks from the saved state, writing the rays
+// still walking below `t_next` lanes to queue r (the last round never
+// stops).  The walk after a resume is the walk that would have run, so
+// every ray's hit boolean is unchanged.  The pixel's count of hits and of
+// rays still out lives in its unused primary-record word (prim[8*pix+7]);
+// the ray that brings the outstanding count to zero writes the pixel.
+// A queue is cut into chunks of kSpillChunk records: a wave takes a whole
+// chunk with one atomic and fills it itself (one atomic per chunk, not per
+// stopped pixel, on the queue's counter), and writes the chunk's fill count
+// when it moves on; a resume wave takes one chunk at a time.
+constexpr int kSpillStack = 10;  // >= the DFS stack (kStack, vrt_kernels.hip)
+constexpr uint32_t kSpillChunk = 256;
+struct alignas(16) SpillRec {
+        uint32_t pix;    // y * W8 + x (primary record index)
+        uint32_t vi;     // y * nx + x (visibility image index)
+        uint32_t sample; // secondary ray index (s_hit)
+        uint32_t sp;     // stack entries
+        float d[3];      // normalised direction (the ray's origin is the pixel's hit point)
+        uint32_t pad;
+        uint32_t base, mask, pad2, pad3;
+        uint32_t stk[2 * kSpillStack];
+};
+static_assert(sizeof(SpillRec) == 128, "SpillRec layout");
+constexpr int kSpillCtrStride = 32;  // one 128-B line per round's counters
+constexpr int kSpillMaxRounds = 4;
+struct SpillQueues {
+        uint32_t *ctr;       // round r: [r*stride + 0] chunks taken by its writers,
+                             // [r*stride + 1] chunks taken by round r+1, [r*stride + 2]
+                             // records written (zeroed per frame)
+        uint32_t *fill[2];   // records in each chunk of queue r (fill[r & 1]), written by the chunk's writer
+        SpillRec *rec[2];    // queue r's records: rec[r & 1] + chunk * kSpillChunk
+        uint32_t nchunks;    // chunks per queue; 0 = no compaction
+        uint32_t t_first;    // phase-A threshold (walking lanes)
+        uint32_t t_next;     // threshold of resume rounds 1..rounds-1
+        int32_t rounds;      // resume launches
+};
+
 // Tile deal of a multi-rank frame.  The ntx x nty grid of
 // 8x8-pixel tiles is cut into G x G blocks of tiles (G = VRT_DEAL_BLOCK);
 // the whole blocks are dealt round-robin in block raster order (block j ->
@@ -462,7 +504,10 @@ hipError_t launch_unpack(int nx, int ny, int ntx, int nty, int nranks,
 hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,
                             int nranks, float res, float *prim, float *vis,
                             int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox,
-                            const WorkQueue *q, hipStream_t st, int *q_waves, int slice_units[8]);
+                            const WorkQueue *q, hipStream_t st, int *q_waves, int slice_units[8],
+                            const SpillQueues *sq = nullptr);
+// the compaction settings of this build (VRT_SEC_SPILL*), cap left 0
+SpillQueues spill_defaults();
 hipError_t launch_light(const LightParams &p, hipStream_t st);
 // samp: n x 6 floats followed by room for their sorted copy (n x 6);
 // seg_start: max_seg entries (>= non-empty leaves), nseg zeroed; seg_end:

@@ -1166,8 +1166,45 @@ __device__ __forceinline__ bool leaf_any(const void *__restrict__ refs, uint32_t
         return false;
 }
 
-template <bool kFast, int kS, bool kR64, bool kFin = false>
-__device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, uint2 *stk)
+// The occlusion walk's state between two node visits: the child block being
+// walked (base), its children still to visit (mask, bit = ci ^ s) and the
+// DFS stack depth (the entries are in the lane's LDS stack column).
+struct OcclState {
+        uint32_t base, mask;
+        int sp;
+};
+enum { kOcclMiss = 0, kOcclHit = 1, kOcclSpill = 2, kOcclWalk = 3 };
+
+// children in ascending (ci ^ s): the near half of each axis first
+__device__ __forceinline__ uint32_t dir_signs(const RayK &r)
+{
+        return (r.d.x < 0.f ? 4u : 0u) | (r.d.y < 0.f ? 2u : 0u) | (r.d.z < 0.f ? 1u : 0u);
+}
+
+// The root: kOcclMiss / kOcclHit when it decides the ray (its box missed, or
+// a leaf root), else kOcclWalk with w = the root's hit children.
+template <bool kFast, bool kR64, bool kFin = false>
+__device__ __forceinline__ int occl_start(const DevScene &sc, const RayK &r, OcclState &w)
+{
+        float bmin[3], bmax[3];
+        uint32_t a, b;
+        load_node(sc.nodes, 0, bmin, bmax, a, b);
+        if (!aabb_isect(bmin, bmax, r.o, r.dinv, r.tmin, r.tmax))
+                return kOcclMiss;
+        if (a & kLeafBit)
+                return leaf_any<kR64>(sc.refs, b, a & ~kLeafBit, r) ? kOcclHit : kOcclMiss;
+        w.mask = xor_permute8(child_hit_mask<kFast, kFin>(bmin, bmax, r) & b, dir_signs(r));
+        w.base = a;
+        w.sp = 0;
+        return kOcclWalk;
+}
+
+// The walk from state w.  kSpill: at each leaf boundary, when fewer than
+// spill_t lanes of the wave are still walking (a wave-uniform decision), the
+// walk stops and returns kOcclSpill with w = where it stopped.
+template <bool kFast, int kS, bool kR64, bool kFin = false, bool kSpill = false>
+__device__ __forceinline__ int occl_walk(const DevScene &sc, const RayK &r, uint2 *stk, OcclState &w,
+                                         uint32_t spill_t = 0)
 {
         float bmin[3], bmax[3];
         uint32_t a, b;
@@ -1176,17 +1213,17 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
         constexpr bool kNB = kLB && VRT_NODE_BOX;  // every visited node by its triangle box
         const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
         const bool lbok = kLB && __all(leaf_box_ok(sc, r));  // wave-uniform: held in SGPRs
-        load_node(sc.nodes, 0, bmin, bmax, a, b);
-        if (!aabb_isect(bmin, bmax, r.o, r.dinv, r.tmin, r.tmax))
-                return false;
-        if (a & kLeafBit)
-                return leaf_any<kR64>(sc.refs, b, a & ~kLeafBit, r);
-        // children in ascending (ci ^ s): the near half of each axis first
-        const uint32_t s = (r.d.x < 0.f ? 4u : 0u) | (r.d.y < 0.f ? 2u : 0u) | (r.d.z < 0.f ? 1u : 0u);
-        uint32_t mask = xor_permute8(child_hit_mask<kFast, kFin>(bmin, bmax, r) & b, s);
-        uint32_t base = a;
-        int sp = 0;
+        const uint32_t s = dir_signs(r);
+        uint32_t mask = w.mask;
+        uint32_t base = w.base;
+        int sp = w.sp;
         for (;;) {
+                if (kSpill && (uint32_t)__popcll(__ballot(1)) < spill_t) {
+                        w.base = base;
+                        w.mask = mask;
+                        w.sp = sp;
+                        return kOcclSpill;
+                }
                 // advance to the next non-empty leaf (while-while, as ray_march)
                 bool leaf = false;
                 uint32_t nref = 0;
@@ -1227,7 +1264,7 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
                         break;
                 }
                 if (!leaf)
-                        return false;
+                        return kOcclMiss;
 #ifndef VRT_SEC_UNI
 #define VRT_SEC_UNI 1
 #endif
@@ -1239,13 +1276,23 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
                         const uint32_t n0 = __builtin_amdgcn_readfirstlane(nref);
                         if (__all(b == f0 && nref == n0)) {
                                 if (leaf_any<true>(static_cast<const RefRec64 *>(sc.refs) + f0, 0, n0, r))
-                                        return true;
+                                        return kOcclHit;
                                 continue;
                         }
                 }
                 if (leaf_any<kR64>(sc.refs, b, nref, r))
-                        return true;
+                        return kOcclHit;
         }
+}
+
+template <bool kFast, int kS, bool kR64, bool kFin = false>
+__device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, uint2 *stk)
+{
+        OcclState w;
+        const int st = occl_start<kFast, kR64, kFin>(sc, r, w);
+        if (st != kOcclWalk)
+                return st == kOcclHit;
+        return occl_walk<kFast, kS, kR64, kFin>(sc, r, stk, w) == kOcclHit;
 }
 
 template <int kS, bool kR64>
@@ -1261,6 +1308,117 @@ __device__ __forceinline__ bool ray_occluded_dispatch(const DevScene &sc, const 
                 return ray_occluded<true, kS, kR64, VRT_FIN != 0>(sc, r, stk);
         return ray_occluded<false, kS, kR64>(sc, r, stk);
 }
+
+// The same walk with compaction (SpillQueues): from the root, or (resume)
+// from the saved state w; returns kOcclMiss / kOcclHit, or kOcclSpill with
+// w = where the walk stopped (fewer than spill_t lanes still walking).  The
+// fast / exact choice is made per wave as in ray_occluded_dispatch; both
+// walks keep the same state (node indices, child masks of the same hit
+// children), so a state saved by one continues in the other.
+template <int kS, bool kR64>
+__device__ __forceinline__ int occl_dispatch_spill(const DevScene &sc, const RayK &r, uint2 *stk, OcclState &w,
+                                                   bool resume, uint32_t spill_t)
+{
+        bool ok = sc.fast_ok && fast_ok(r);
+        if (VRT_FIN)
+                ok = ok && fin_ok(r);
+        if (__all(ok)) {
+                if (!resume) {
+                        const int st = occl_start<true, kR64, VRT_FIN != 0>(sc, r, w);
+                        if (st != kOcclWalk)
+                                return st;
+                }
+                return occl_walk<true, kS, kR64, VRT_FIN != 0, true>(sc, r, stk, w, spill_t);
+        }
+        if (!resume) {
+                const int st = occl_start<false, kR64>(sc, r, w);
+                if (st != kOcclWalk)
+                        return st;
+        }
+        return occl_walk<false, kS, kR64, false, true>(sc, r, stk, w, spill_t);
+}
+
+// One stopped ray's record (SpillRec): its pixel, sample, direction and walk
+// state, the stack entries copied out of the lane's LDS column.
+template <int kS>
+__device__ __forceinline__ void spill_write(SpillRec *o, uint32_t pix, uint32_t vi, uint32_t sample, f3 d,
+                                            const OcclState &w, const uint2 *stk)
+{
+        uint4 *q = reinterpret_cast<uint4 *>(o);
+        q[0] = make_uint4(pix, vi, sample, (uint32_t)w.sp);
+        q[1] = make_uint4(__float_as_uint(d.x), __float_as_uint(d.y), __float_as_uint(d.z), 0u);
+        q[2] = make_uint4(w.base, w.mask, 0u, 0u);
+        uint2 *e = reinterpret_cast<uint2 *>(o->stk);
+        for (int k = 0; k < w.sp; ++k)
+                e[k] = stk[k * kS];
+}
+
+// lane 0 adds n to *ctr, the wave reads lane 0's result (as take_unit)
+__device__ __forceinline__ uint32_t take_n(uint32_t *ctr, uint32_t n)
+{
+        int lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        const uint32_t old = atomicAdd(ctr, lane == 0 ? n : 0u);
+        return __builtin_amdgcn_readlane(old, 0);
+}
+
+// A wave's place in a compaction queue (SpillQueues): the chunk it fills and
+// the records in it so far (wave-uniform).
+constexpr uint32_t kSpillNone = 0xFFFFFFFFu;  // no chunk yet
+constexpr uint32_t kSpillFull = 0xFFFFFFFEu;  // the queue has no chunk left
+struct SpillCursor {
+        uint32_t chunk, fill;
+};
+
+// The chunk's fill count, for the round that reads the queue, and the
+// queue's record total (ctr[2], vrt_secondary_spill_counts).  Every lane
+// active: the total is one folded whole-wave add (as take_unit).
+__device__ __forceinline__ void spill_close(uint32_t *fills, uint32_t *ctr, const SpillCursor &c)
+{
+        if (c.chunk >= kSpillFull)
+                return;
+        int lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        if (lane == 0)
+                fills[c.chunk] = c.fill;
+        atomicAdd(ctr + 2, lane == 0 ? c.fill : 0u);
+}
+
+// Before a group of up to 64 rays (every lane active, wave-uniform): room
+// for 64 more records in the cursor's chunk, taking the queue's next chunk
+// if needed.  Returns the stop threshold the group may use: t, or 0 (no
+// compaction, or the queue is full).
+__device__ __forceinline__ uint32_t spill_reserve(const SpillQueues &q, uint32_t *ctr, uint32_t *fills,
+                                                  SpillCursor &c, uint32_t t)
+{
+        if (q.nchunks == 0 || t == 0 || c.chunk == kSpillFull)
+                return 0u;
+        if (c.chunk != kSpillNone && c.fill + 64u <= kSpillChunk)
+                return t;
+        spill_close(fills, ctr, c);
+        const uint32_t k = take_n(ctr, 1u);
+        c.chunk = k < q.nchunks ? k : kSpillFull;
+        c.fill = 0;
+        return c.chunk == kSpillFull ? 0u : t;
+}
+
+// The stopped rays of a group (`spilled`, after the walks): each writes its
+// record at the cursor's next free slots in lane order.
+template <int kS>
+__device__ __forceinline__ void spill_group(SpillRec *rec, SpillCursor &c, bool spilled, uint32_t pix, uint32_t vi,
+                                            uint32_t sample, f3 d, const OcclState &w, const uint2 *stk)
+{
+        const uint64_t sm = __ballot(spilled);
+        if (sm == 0)
+                return;
+        if (spilled) {
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+                spill_write<kS>(rec + (size_t)c.chunk * kSpillChunk + c.fill + below, pix, vi, sample, d, w, stk);
+        }
+        c.fill += (uint32_t)__popcll(sm);
+}
+
 
 // Triangle::get_albedo (VRT/voxel_octree.cc:472-484) with Triangle::isect's
 // normal (VRT/voxel_octree.cc:451-453).
@@ -1777,12 +1935,13 @@ struct SecondaryParams {
         int32_t nx, W8, H8, spp;
         int32_t rank, nranks;  // this rank's 8x8 tiles: tile_deal
         float res;
-        const float *prim;
+        float *prim;           // 8 floats per pixel: k_primary1's record, [7] the compaction counts
         float *vis;            // nx*ny, this rank's pixels written
         int32_t *s_hit, *s_tri;
         uint32_t *s_vox;
         int32_t units;         // this rank's pixels (persistent launch)
         WorkQueue q;           // persistent launch only
+        SpillQueues sq;        // ray compaction (kAny, persistent launch); sq.nchunks == 0: off
 };
 
 #ifndef VRT_SEC_WAVES
@@ -1792,6 +1951,11 @@ struct SecondaryParams {
 #define VRT_SEC_WAVES_PER_EU 6
 #endif
 constexpr int kSecBlock = 64 * VRT_SEC_WAVES;
+// the persistent config-5 kernels (k_secondary_p, k_sec_resume): 4-wave workgroups
+constexpr int kSecPBlock = 256;
+#ifndef VRT_SECP_WAVES_PER_EU
+#define VRT_SECP_WAVES_PER_EU 6
+#endif
 
 // One pixel of config 5: this rank's k-th pixel (pixel k % 64 of its tile
 // k / 64), the wave's 64 lanes = its secondary rays.
@@ -1800,7 +1964,7 @@ constexpr int kSecBlock = 64 * VRT_SEC_WAVES;
 // ray's hit boolean -> the occlusion walk (ray_occluded), same booleans.
 template <bool kR64, bool kAny, int kS>
 __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_t k, int lane, uint2 *stk,
-                                                float (*pts)[3])
+                                                float (*pts)[3], SpillCursor &cur)
 {
         // lane id re-read per pixel (not held across k_secondary_p's loop)
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
@@ -1852,15 +2016,22 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        bool hit = false;
+        // with compaction: the rays still walking when fewer than t_first
+        // lanes are go to queue 0 (SpillQueues)
+        const uint32_t t = kAny ? spill_reserve(p.sq, p.sq.ctr, p.sq.fill[0], cur, p.sq.t_first) : 0u;
+        bool hit = false, spilled = false;
+        OcclState w;
+        f3 dn;
         if (lane < p.spp) {
                 const f3 pt = mk3(pts[lane][0], pts[lane][1], pts[lane][2]);
-                const f3 dn = normalize(nrm + pt);  // Ray{hit, n + p, res} normalises d
+                dn = normalize(nrm + pt);  // Ray{hit, n + p, res} normalises d
                 const RayK r = make_rayk(hp, dn, p.res, kFltMax);
                 const size_t si = vi * (size_t)p.spp + lane;
                 if (kAny) {
-                        hit = ray_occluded_dispatch<kS, kR64>(p.sc, r, stk);
-                        if (p.s_hit) p.s_hit[si] = hit ? 1 : 0;
+                        const int res = occl_dispatch_spill<kS, kR64>(p.sc, r, stk, w, false, t);
+                        hit = res == kOcclHit;
+                        spilled = res == kOcclSpill;
+                        if (p.s_hit && !spilled) p.s_hit[si] = hit ? 1 : 0;
                 } else {
                         MarchResult m;
                         ray_march_dispatch<false, kS, false, kR64>(p.sc, r, stk, nullptr, nullptr, m);
@@ -1870,9 +2041,105 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
                         if (p.s_vox) p.s_vox[si] = m.hit ? p.sc.node_vox[m.node] : 0xFFFFFFFFu;
                 }
         }
+        if (kAny && t)
+                spill_group<kS>(p.sq.rec[0], cur, spilled, (uint32_t)pix, (uint32_t)vi, (uint32_t)lane, dn, w, stk);
         const uint64_t hm = __ballot(hit);
-        if (lane == 0)
-                p.vis[vi] = (float)(p.spp - (int)__popcll(hm)) / (float)p.spp;
+        const uint64_t sm = kAny ? __ballot(spilled) : 0ull;
+        if (lane == 0) {
+                if (sm == 0)
+                        p.vis[vi] = (float)(p.spp - (int)__popcll(hm)) / (float)p.spp;
+                else  // hits so far << 8 | rays still out: the resume rounds finish the pixel
+                        reinterpret_cast<uint32_t *>(p.prim + 8 * pix)[7] =
+                                ((uint32_t)__popcll(hm) << 8) | (uint32_t)__popcll(sm);
+        }
+}
+
+// Resume round p.round of the compaction (SpillQueues): queue round-1's rays,
+// 64 to a wave in append order, walk on from their saved states; a ray that
+// ends adds to its pixel's counts (prim[8*pix+7]: hits << 8 | rays out) and
+// the one that brings the rays out to zero writes the pixel; below t_next
+// walking lanes (not in the last round) a ray goes to queue round.
+struct ResumeParams {
+        DevScene sc;
+        float *prim;
+        float *vis;
+        int32_t *s_hit;
+        int32_t spp;
+        float res;
+        int32_t round;
+        SpillQueues sq;
+};
+
+// One chunk of queue round-1: its rays 64 at a time, each walk continued
+// from its record; rays that end update their pixel, rays stopped again (t >
+// 0, not the last round) go to queue round.
+template <bool kR64>
+__device__ __forceinline__ void resume_chunk(const ResumeParams &p, const SpillRec *rec, uint32_t fill, uint32_t t,
+                                             SpillCursor &cur, uint2 *stk)
+{
+        uint32_t *cout = p.sq.ctr + p.round * kSpillCtrStride;
+        uint32_t *fout = p.sq.fill[p.round & 1];
+        for (uint32_t g = 0; g < fill; g += 64) {
+                const uint32_t tg = spill_reserve(p.sq, cout, fout, cur, t);
+                int lane;
+                asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+                const uint32_t i = g + (uint32_t)lane;
+                bool spilled = false;
+                OcclState w;
+                f3 dn;
+                uint4 h0 = make_uint4(0u, 0u, 0u, 0u);
+                if (i < fill) {
+                        const SpillRec *q = rec + i;
+                        h0 = reinterpret_cast<const uint4 *>(q)[0];
+                        const uint4 h1 = reinterpret_cast<const uint4 *>(q)[1];
+                        const uint4 h2 = reinterpret_cast<const uint4 *>(q)[2];
+                        w.sp = (int)h0.w;
+                        w.base = h2.x;
+                        w.mask = h2.y;
+                        const uint2 *e = reinterpret_cast<const uint2 *>(q->stk);
+                        for (int k = 0; k < w.sp; ++k)
+                                stk[k * kSecPBlock] = e[k];
+                        float *pr = p.prim + 8 * (size_t)h0.x;
+                        const f3 hp = mk3(pr[1], pr[2], pr[3]);
+                        dn = mk3(__uint_as_float(h1.x), __uint_as_float(h1.y), __uint_as_float(h1.z));
+                        const RayK r = make_rayk(hp, dn, p.res, kFltMax);
+                        const int res = occl_dispatch_spill<kSecPBlock, kR64>(p.sc, r, stk, w, true, tg);
+                        spilled = res == kOcclSpill;
+                        if (!spilled) {
+                                const uint32_t hit = res == kOcclHit ? 1u : 0u;
+                                if (p.s_hit)
+                                        p.s_hit[(size_t)h0.y * (size_t)p.spp + h0.z] = (int32_t)hit;
+                                const uint32_t old =
+                                        atomicAdd(reinterpret_cast<uint32_t *>(pr) + 7, hit ? 255u : 0xFFFFFFFFu);
+                                if ((old & 0xFFu) == 1u)  // the pixel's last ray
+                                        p.vis[h0.y] = (float)(p.spp - (int)((old >> 8) + hit)) / (float)p.spp;
+                        }
+                }
+                if (tg)
+                        spill_group<kSecPBlock>(p.sq.rec[p.round & 1], cur, spilled, h0.x, h0.y, h0.z, dn, w, stk);
+        }
+}
+
+template <bool kR64>
+__global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_resume(ResumeParams p)
+{
+        __shared__ uint2 stk[kStack * kSecPBlock];
+        const int tid = threadIdx.x;
+        uint32_t *cin = p.sq.ctr + (p.round - 1) * kSpillCtrStride;
+        const uint32_t n = min(cin[0], p.sq.nchunks);  // queue round-1's chunks (earlier launches)
+        const uint32_t *fin = p.sq.fill[(p.round - 1) & 1];
+        const SpillRec *in = p.sq.rec[(p.round - 1) & 1];
+        const uint32_t t = p.round < p.sq.rounds ? p.sq.t_next : 0u;
+        SpillCursor cur;
+        cur.chunk = kSpillNone;
+        cur.fill = 0;
+        for (;;) {
+                const uint32_t c = take_n(cin + 1, 1u);
+                if (c >= n)
+                        break;
+                resume_chunk<kR64>(p, in + (size_t)c * kSpillChunk, fin[c], t, cur, stk + tid);
+        }
+        spill_close(p.sq.fill[p.round & 1], p.sq.ctr + p.round * kSpillCtrStride, cur);
 }
 
 template <bool kR64, bool kAny>
@@ -1882,7 +2149,10 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
         __shared__ float pts[VRT_SEC_WAVES][64][3];
         const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
         const int64_t k = (int64_t)blockIdx.x * VRT_SEC_WAVES + wave;
-        secondary_pixel<kR64, kAny, kSecBlock>(p, k, lane, stk + tid, pts[wave]);
+        SpillCursor cur;  // no compaction in the one-pixel-per-wave grid (p.sq.nchunks == 0)
+        cur.chunk = kSpillNone;
+        cur.fill = 0;
+        secondary_pixel<kR64, kAny, kSecBlock>(p, k, lane, stk + tid, pts[wave], cur);
 }
 
 // Persistent config 5: one resident generation of 4-wave workgroups; each
@@ -1890,10 +2160,6 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
 // WorkQueue (XCD x owns a contiguous slice of this rank's pixels, then
 // helps the others), so no wave waits for a slow pixel of a sibling and the
 // resident-wave count is not capped by the per-CU workgroup limit.
-constexpr int kSecPBlock = 256;
-#ifndef VRT_SECP_WAVES_PER_EU
-#define VRT_SECP_WAVES_PER_EU 6
-#endif
 template <bool kR64, bool kAny>
 __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary_p(SecondaryParams p)
 {
@@ -1901,6 +2167,9 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
         __shared__ float pts[kSecPBlock / 64][64][3];
         const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
         const int xcd = blockIdx.x & 7;
+        SpillCursor cur;
+        cur.chunk = kSpillNone;
+        cur.fill = 0;
         for (int j = 0; j < 8; ++j) {
                 const int x = (xcd + j) & 7;
                 const int n = slice_size(p.units, x, VRT_SEC_SLICE_CHUNK);
@@ -1912,14 +2181,39 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
                                 break;
                         secondary_pixel<kR64, kAny, kSecPBlock>(
                                 p, (int64_t)slice_unit(p.units, x, (int)u, VRT_SEC_SLICE_CHUNK), lane, stk + tid,
-                                pts[wave]);
+                                pts[wave], cur);
                 }
         }
+        if (kAny)
+                spill_close(p.sq.fill[0], p.sq.ctr, cur);
+}
+
+#ifndef VRT_SEC_SPILL_T
+#define VRT_SEC_SPILL_T 24    // phase A stops below this many walking lanes (0: no compaction)
+#endif
+#ifndef VRT_SEC_SPILL_T2
+#define VRT_SEC_SPILL_T2 24   // the same in resume rounds before the last
+#endif
+#ifndef VRT_SEC_ROUNDS
+#define VRT_SEC_ROUNDS 3      // resume launches
+#endif
+static_assert(VRT_SEC_ROUNDS >= 1 && VRT_SEC_ROUNDS < kSpillMaxRounds, "VRT_SEC_ROUNDS");
+static_assert(kSpillStack >= kStack, "SpillRec stack");
+
+SpillQueues spill_defaults()
+{
+        SpillQueues q;
+        std::memset(&q, 0, sizeof q);
+        q.t_first = VRT_SEC_SPILL_T;
+        q.t_next = VRT_SEC_SPILL_T2;
+        q.rounds = VRT_SEC_ROUNDS;
+        return q;
 }
 
 hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nranks, float res,
                             float *prim, float *vis, int32_t *s_hit, int32_t *s_tri,
-                            uint32_t *s_vox, const WorkQueue *q, hipStream_t st, int *q_waves, int slice_units[8])
+                            uint32_t *s_vox, const WorkQueue *q, hipStream_t st, int *q_waves, int slice_units[8],
+                            const SpillQueues *sq)
 {
         *q_waves = 0;
         for (int x = 0; x < 8; ++x)
@@ -1963,10 +2257,37 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                 const int g = (int)std::min<int64_t>(cap, ((waves + 3) / 4 + 7) & ~7LL);
                 void (*kern)(SecondaryParams) = w ? (any ? k_secondary_p<true, true> : k_secondary_p<true, false>)
                                                   : (any ? k_secondary_p<false, true> : k_secondary_p<false, false>);
+                const bool spill = any && sq && sq->t_first > 0 && sq->nchunks > 0;
+                if (spill) {
+                        sp.sq = *sq;
+                        if (rp.test_flags & VRT_TEST_SPILL_ALL)  // test hook: stop at the first ray's end
+                                sp.sq.t_first = sp.sq.t_next = 64;
+                }
                 hipLaunchKernelGGL(kern, dim3(g), dim3(kSecPBlock), 0, st, sp);
                 *q_waves = g * (kSecPBlock / 64);
                 for (int x = 0; x < 8; ++x)
                         slice_units[x] = slice_size((int)waves, x, VRT_SEC_SLICE_CHUNK);
+                if (hipError_t e = hipGetLastError())
+                        return e;
+                if (spill) {
+                        // resume rounds: one resident generation each, every
+                        // wave taking 64 records at a time until the queue is
+                        // drained (an empty queue ends the launch at once)
+                        ResumeParams rp2;
+                        std::memset(&rp2, 0, sizeof rp2);
+                        rp2.sc = rp.sc;
+                        rp2.prim = prim;
+                        rp2.vis = vis;
+                        rp2.s_hit = s_hit;
+                        rp2.spp = spp;
+                        rp2.res = res;
+                        rp2.sq = sp.sq;
+                        for (int r = 1; r <= sp.sq.rounds; ++r) {
+                                rp2.round = r;
+                                hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(g),
+                                                   dim3(kSecPBlock), 0, st, rp2);
+                        }
+                }
                 return hipGetLastError();
         }
         void (*kern)(SecondaryParams) = w ? (any ? k_secondary<true, true> : k_secondary<true, false>)
