@@ -781,9 +781,11 @@ def main():
             ks = pmc.get("kernel_stats") or {}
             cand = [k for k in pk if not k.startswith(HELPERS) and "SQ_INSTS_VALU" in pk[k] and "FETCH_SIZE" in pk[k]
                     and "vrt::" in pmc["dispatch"].get(k, {}).get("kernel", "")]
-            if trace:
-                # the full frame's kernels, each against its own rocprof time;
-                # the line's roofline = the one with the most time per frame
+            if trace or secondary:
+                # the frame's kernels (trace: light pass, light map, render;
+                # config 5: primary hits, the secondary walk and its resume
+                # rounds), each against its own rocprof time; the line's
+                # roofline = the one with the most time per frame
                 trace_kernels = {}
                 for k in cand:
                     if k in ks:
@@ -796,7 +798,7 @@ def main():
                 dom = max(trace_kernels, key=lambda k: trace_kernels[k]["time_basis"]["rocprof_ms_per_frame"]) \
                     if trace_kernels else None
                 roof = dict(trace_kernels[dom]) if dom else None
-                if roof:
+                if roof and trace:
                     roof["traffic_over_output"] = None  # the frame writes only the 1024^2 image
             else:
                 dom = max(cand, key=lambda k: pk[k]["SQ_INSTS_VALU"]) if cand else None
@@ -999,6 +1001,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if secondary and trace_kernels:
+            out["roofline_per_kernel"] = trace_kernels
         if d9:
             out["depth_plus1"] = d9
         if host_out:

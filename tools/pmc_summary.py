@@ -33,7 +33,7 @@ def main():
     m = per[kern]
     child_ms = m["GRBM_GUI_ACTIVE"] / 8 / (r["clock_ghz_profiled"] * 1e9) * 1e3
     pmc = {"per_kernel": per, "dispatch": meta, "kernel_stats": stats, "child_kernel_ms": child_ms}
-    if mode == "trace":
+    if "rocprof_ms_per_frame" in tb:  # trace / config 5: per-kernel rocprof time per frame
         t = tb["rocprof_ms_per_frame"]
         again = bench.roofline_from_pmc(pmc, kern, t, out_bytes, None, child_ms=child_ms)
     else:
