@@ -790,9 +790,16 @@ def main():
                 for k in cand:
                     if k in ks:
                         calls, avg, tot = ks[k]
-                        r_ = roofline_from_pmc(pmc, k, tot / a.steps, out_bytes, None, child_ms=tot / a.steps)
-                        r_["time_basis"] = {"rocprof_ms_per_frame": round(tot / a.steps, 4),
-                                            "dispatches_per_frame": round(calls / a.steps, 2),
+                        # the timed frames' dispatches of k per frame (the
+                        # PMC pass counts them; config 5 also renders each
+                        # pose once untimed for its ray count) x the
+                        # kernel-trace average duration
+                        per = pmc["per_frame_dispatches"].get(k) or calls / a.steps
+                        fms = avg * per
+                        r_ = roofline_from_pmc(pmc, k, fms, out_bytes, None, child_ms=fms)
+                        r_["time_basis"] = {"rocprof_ms_per_frame": round(fms, 4),
+                                            "dispatches_per_frame": round(per, 2),
+                                            "rocprof_avg_ms": round(avg, 4), "rocprof_calls": calls,
                                             "note": "rocprofv3 kernel trace of this command (one frame in flight)"}
                         trace_kernels[k] = r_
                 dom = max(trace_kernels, key=lambda k: trace_kernels[k]["time_basis"]["rocprof_ms_per_frame"]) \
