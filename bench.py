@@ -362,8 +362,9 @@ def parse():
                         "unpacks; from 4 ranks on the deal gives it fewer tiles than the others)")
     p.add_argument("--rehearse-render-only", action="store_true",
                    help="with --rehearse-ranks: time the share's renders alone (no gather, no unpack)")
-    p.add_argument("--frames-in-flight-secondary", type=int, default=1,
-                   help="frames in flight for --mode secondary (36 ms frames: 2 in flight measured 5%% slower)")
+    p.add_argument("--frames-in-flight-secondary", type=int, default=3,
+                   help="frames in flight for --mode secondary (with the ray compaction's resume tails: "
+                        "1 / 2 / 3 in flight 18.86 / 18.64 / 18.49 ms per frame, round 3)")
     p.add_argument("--rehearse-ranks", type=int, default=0,
                    help="single-GPU rehearsal of the N-rank path (WORLD_SIZE 1): render rank 0's share of the "
                         "tiles as one of R ranks, RCCL gather over a 1-rank process group, unpack of R rank "

@@ -340,10 +340,15 @@ struct vrt_scene {
         void *d_trace = nullptr;  // split-trace scratch (records + colours)
         size_t trace_bytes = 0;
         // config-5 ray compaction (SpillQueues): round counters + two record
-        // queues of spill_cap records each
-        void *d_spill = nullptr;
-        uint32_t spill_cap = 0;   // chunks per queue
-        bool spill_used = false;  // the last config-5 launch compacted (vrt_secondary_spill_counts)
+        // queues of spill_cap chunks each; two sets, used by alternate
+        // frames (two config-5 frames in flight on two streams), each with
+        // the event of its last launch
+        void *d_spill[2] = {};
+        uint32_t spill_cap[2] = {};  // chunks per queue
+        hipEvent_t spill_ev[2] = {};
+        bool spill_live[2] = {};
+        int spill_next = 0;
+        int spill_last = -1;  // the set the last config-5 launch compacted with (vrt_secondary_spill_counts)
         // device
         void *d_mem = nullptr;
         DevScene dev{};
@@ -994,7 +999,8 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
 {
         if (!s)
                 return;
-        if (s->d_mem || s->d_lm || s->d_light || s->d_trace || s->d_spill || s->stream || s->ev0 || s->ev1 ||
+        if (s->d_mem || s->d_lm || s->d_light || s->d_trace || s->d_spill[0] || s->d_spill[1] || s->stream || s->ev0 ||
+            s->ev1 ||
             s->scratch_ev) {
                 (void)hipSetDevice(s->device);
                 if (s->stream)
@@ -1007,8 +1013,12 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                         (void)hipFree(s->d_light);
                 if (s->d_trace)
                         (void)hipFree(s->d_trace);
-                if (s->d_spill)
-                        (void)hipFree(s->d_spill);
+                for (int k = 0; k < 2; ++k) {
+                        if (s->d_spill[k])
+                                (void)hipFree(s->d_spill[k]);
+                        if (s->spill_ev[k])
+                                (void)hipEventDestroy(s->spill_ev[k]);
+                }
                 if (s->ev0)
                         (void)hipEventDestroy(s->ev0);
                 if (s->ev1)
@@ -1264,45 +1274,54 @@ static int scratch_release(vrt_scene *s, hipStream_t st);
 // Compaction queues of one config-5 launch (SpillQueues): room
 // for every secondary ray of this rank, in chunks, up to kSpillCapMax records
 // per queue (a full queue only means the rays beyond it finish in their
-// first wave); the round counters zeroed on the stream.  The buffers are
-// scene scratch: the launch holds them through scratch_acquire /
-// scratch_release.  sq->nchunks stays 0 (no compaction) when the build
-// disables it or the allocation fails.
+// first wave); the round counters zeroed on the stream.  The scene keeps two
+// sets, taken by alternate launches (two frames in flight on two streams);
+// a set's next user waits for the event of its last.  sq->nchunks stays 0
+// (no compaction) when the build disables it or the allocation fails.
 constexpr uint32_t kSpillCapMax = 1u << 24;  // 2 GiB of records per queue
-static int spill_setup(vrt_scene *s, int64_t rays, hipStream_t st, SpillQueues *sq)
+static int spill_setup(vrt_scene *s, int64_t rays, hipStream_t st, SpillQueues *sq, int *set)
 {
         *sq = spill_defaults();
+        *set = -1;
         if (sq->t_first == 0 || rays <= 0)
                 return VRT_OK;
+        // the next of the two sets; this stream first waits for its last user
+        const int k = s->spill_next;
+        s->spill_next ^= 1;
+        if (!s->spill_ev[k])
+                HIPCHK(hipEventCreateWithFlags(&s->spill_ev[k], hipEventDisableTiming));
+        if (s->spill_live[k])
+                HIPCHK(hipStreamWaitEvent(st, s->spill_ev[k], 0));
         // + one partly filled chunk per wave of a resident grid
         const int64_t want = rays + (int64_t)std::max(1, s->dev.sec_blocks) * 4 * kSpillChunk;
         const uint32_t nch = (uint32_t)((std::min<int64_t>(want, kSpillCapMax) + kSpillChunk - 1) / kSpillChunk);
         const size_t ctr_bytes = (size_t)kSpillMaxRounds * kSpillCtrStride * 4;
         const size_t fill_bytes = ((size_t)nch * 4 + 255) & ~(size_t)255;
-        if (s->spill_cap < nch) {
-                if (s->d_spill) {
+        if (s->spill_cap[k] < nch) {
+                if (s->d_spill[k]) {
                         HIPCHK(hipDeviceSynchronize());  // earlier launches on any stream may use it
-                        (void)hipFree(s->d_spill);
-                        s->d_spill = nullptr;
-                        s->spill_cap = 0;
+                        (void)hipFree(s->d_spill[k]);
+                        s->d_spill[k] = nullptr;
+                        s->spill_cap[k] = 0;
                 }
-                if (hipMalloc(&s->d_spill, ctr_bytes + 2 * fill_bytes + 2 * (size_t)nch * kSpillChunk * sizeof(SpillRec)) !=
+                if (hipMalloc(&s->d_spill[k], ctr_bytes + 2 * fill_bytes + 2 * (size_t)nch * kSpillChunk * sizeof(SpillRec)) !=
                     hipSuccess) {
                         (void)hipGetLastError();
-                        s->d_spill = nullptr;
+                        s->d_spill[k] = nullptr;
                         return VRT_OK;  // no compaction
                 }
-                s->spill_cap = nch;
+                s->spill_cap[k] = nch;
         }
-        const size_t fb = ((size_t)s->spill_cap * 4 + 255) & ~(size_t)255;
-        char *b = static_cast<char *>(s->d_spill);
+        const size_t fb = ((size_t)s->spill_cap[k] * 4 + 255) & ~(size_t)255;
+        char *b = static_cast<char *>(s->d_spill[k]);
         sq->ctr = reinterpret_cast<uint32_t *>(b);
         sq->fill[0] = reinterpret_cast<uint32_t *>(b + ctr_bytes);
         sq->fill[1] = reinterpret_cast<uint32_t *>(b + ctr_bytes + fb);
         sq->rec[0] = reinterpret_cast<SpillRec *>(b + ctr_bytes + 2 * fb);
-        sq->rec[1] = sq->rec[0] + (size_t)s->spill_cap * kSpillChunk;
-        sq->nchunks = s->spill_cap;
+        sq->rec[1] = sq->rec[0] + (size_t)s->spill_cap[k] * kSpillChunk;
+        sq->nchunks = s->spill_cap[k];
         HIPCHK(hipMemsetAsync(sq->ctr, 0, ctr_bytes, st));
+        *set = k;
         return VRT_OK;
 }
 
@@ -1317,24 +1336,24 @@ static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int ra
         (void)hipGetLastError();  // a leftover error of an earlier call is not this launch's
         SpillQueues sq;
         std::memset(&sq, 0, sizeof sq);
+        int set = -1;
         if (secondary_uses_queue(p.sc)) {
                 if (int rc = queue_take(s, st, &q, &slot))
                         return rc;
                 if (!s_tri && !s_vox) {  // the occlusion walk: compaction
                         const int64_t rays = deal_count(tile_deal(p.ntx, p.nty, nranks), rank) * 64 * (int64_t)spp;
-                        if (int rc = scratch_acquire(s, st))
-                                return rc;
-                        if (int rc = spill_setup(s, rays, st, &sq))
+                        if (int rc = spill_setup(s, rays, st, &sq, &set))
                                 return rc;
                 }
         }
         int waves = 0, units[8];
-        s->spill_used = sq.nchunks > 0;
+        s->spill_last = sq.nchunks > 0 ? set : -1;
         const hipError_t e = launch_secondary(p, spp, rank, nranks, scene_res(s), d_prim, d_vis, s_hit, s_tri,
                                               s_vox, slot >= 0 ? &q : nullptr, st, &waves, units, &sq);
-        if (sq.nchunks > 0)
-                if (int rc = scratch_release(s, st))
-                        return rc;
+        if (set >= 0) {
+                HIPCHK(hipEventRecord(s->spill_ev[set], st));
+                s->spill_live[set] = true;
+        }
         if (e != hipSuccess) {
                 if (slot >= 0)
                         queue_reset(s, slot, st);
@@ -1707,12 +1726,12 @@ extern "C" int vrt_secondary_spill_counts(vrt_scene *s, int64_t counts[4])
         std::lock_guard<std::mutex> lk(s->mu);
         for (int r = 0; r < 4; ++r)
                 counts[r] = 0;
-        if (!s->spill_used || !s->d_spill)
+        if (s->spill_last < 0 || !s->d_spill[s->spill_last])
                 return VRT_OK;
         HIPCHK(hipSetDevice(s->device));
         HIPCHK(hipDeviceSynchronize());
         std::vector<uint32_t> c((size_t)kSpillMaxRounds * kSpillCtrStride);
-        HIPCHK(hipMemcpy(c.data(), s->d_spill, c.size() * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(c.data(), s->d_spill[s->spill_last], c.size() * 4, hipMemcpyDeviceToHost));
         for (int r = 0; r < 4 && r < kSpillMaxRounds; ++r)
                 counts[r] = c[(size_t)r * kSpillCtrStride + 2];  // records (spill_close)
         return VRT_OK;
