@@ -159,7 +159,8 @@ def run_pmc(a, save_dir=""):
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     child = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-counters", "--no-pmc", "--no-d9",
-             "--frames-in-flight", "1", "--warmup", "0", "--steps", str(a.steps), *workload_args(a)]
+             "--frames-in-flight", "1", "--frames-in-flight-secondary", "1", "--warmup", "0", "--steps",
+             str(a.steps), *workload_args(a)]
     per, nd, meta, child_ms, skipped = {}, {}, {}, {}, []
     stats = None
     passes = [(n, ["--pmc", *c], opt) for n, c, opt in PMC_PASSES] + [("ktrace", ["--kernel-trace", "--stats"], False)]
