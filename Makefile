@@ -17,7 +17,7 @@ HIPFLAGS := -x hip --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 $(FP) -Iinclude -
 CXXFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Wall -fvisibility=hidden
 
 LIBS := -L/opt/rocm/lib -lrccl -lpthread
-HOSTOBJS := $(BLD)/vrt_host.o $(BLD)/vrt_multi.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o
+HOSTOBJS := $(BLD)/vrt_host.o $(BLD)/vrt_legacy.o $(BLD)/vrt_multi.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o
 OBJS := $(BLD)/vrt_kernels.o $(BLD)/vrt_build.o $(HOSTOBJS) $(BLD)/vrt_build_id.o
 HDRS := include/vrt.h $(SRC)/vrt_math.h $(SRC)/vrt_internal.h $(SRC)/vrt_error.h
 
@@ -37,6 +37,11 @@ $(BLD)/vrt_build.o: $(SRC)/vrt_build.hip $(HDRS) | $(BLD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BLD)/vrt_host.o: $(SRC)/vrt_host.cpp $(HDRS) | $(BLD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# the reference's primitives under their C++ (mangled) names; must not see
+# vrt.h's extern "C" declarations of the same signatures
+$(BLD)/vrt_legacy.o: $(SRC)/vrt_legacy.cpp $(SRC)/vrt_math.h | $(BLD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 # the multi-device frame: RCCL (ncclCommInitAll + ncclGather over xGMI)
@@ -79,12 +84,12 @@ variant: $(HOSTOBJS) $(BLD)/vrt_build.o | $(BLD)
 	  build/variants/k_$(NAME).o $(BLD)/vrt_build.o $(HOSTOBJS) $(BLD)/vrt_build_id.o $(LIBS)
 
 # variant that also rebuilds the host side (for data-layout changes)
-fullvariant: $(BLD)/vrt_build.o $(BLD)/vrt_multi.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o | $(BLD)
+fullvariant: $(BLD)/vrt_build.o $(BLD)/vrt_legacy.o $(BLD)/vrt_multi.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o | $(BLD)
 	mkdir -p build/variants
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_host.cpp -o build/variants/h_$(NAME).o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
-	  build/variants/k_$(NAME).o build/variants/h_$(NAME).o $(BLD)/vrt_build.o $(BLD)/vrt_multi.o \
+	  build/variants/k_$(NAME).o build/variants/h_$(NAME).o $(BLD)/vrt_build.o $(BLD)/vrt_legacy.o $(BLD)/vrt_multi.o \
 	  $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o $(BLD)/vrt_build_id.o $(LIBS)
 
 # ISA listing + register/occupancy report of the kernels (for DESIGN.md)

@@ -371,6 +371,9 @@ int64_t vrt_write_hdr_rgbe_mem(int w, int h, const uint8_t *rgbe,
                                uint8_t *out, int64_t cap);
 
 /* ---- legacy reference symbols (identical signatures and results) ------- */
+/* C linkage here; the library also defines the same two functions with the
+ * reference headers' C++ linkage (declared in vrt_legacy.hpp), the names
+ * VRT/voxel_octree.cc:446,490 import. */
 /* VRT/raytri.h:5-7 */
 int intersect_triangle3(double orig[3], double dir[3], double vert0[3],
                         double vert1[3], double vert2[3], double *t,

@@ -39,6 +39,10 @@ def test_no_unexpected_exports():
     exported = {ln.split()[-1] for ln in out if " T " in ln}
     extra = {e for e in exported if not e.startswith("_Z")} - set(declared_functions())
     assert not extra, extra
+    # the only C++ (mangled) exports are the reference's two primitives,
+    # declared in include/vrt_legacy.hpp (VRT/raytri.h:5-7, VRT/tribox2.h:6)
+    mangled = {e for e in exported if e.startswith("_Z")}
+    assert mangled == {"_Z19intersect_triangle3PdS_S_S_S_S_S_S_", "_Z13triBoxOverlapPfS_PA3_f"}, mangled
 
 
 CAMS = [

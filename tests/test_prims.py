@@ -5,12 +5,16 @@ The golden KATs were produced by the reference's own raytri.cc / tribox2.cc
 (2) the product's legacy C symbols intersect_triangle3 / triBoxOverlap, which
 run the exact code the kernels inline (csrc/vrt_math.h).  Bit-exact.
 """
+import os
+import shutil
+import subprocess
+
 import numpy as np
 import pytest
 
 import pyoracle as po
 import voxelraytrace20190722_amd as vrt
-from conftest import golden
+from conftest import ROOT, golden
 
 
 def _mt_all(fn, q):
@@ -62,3 +66,42 @@ def test_live_random_vs_reference():
         b = rng.standard_normal(15).astype(np.float32)
         b[3:6] = np.abs(b[3:6])
         assert po.ref_tri_box_overlap(b) == vrt.tri_box_overlap(b[0:3], b[3:6], b[6:15])
+
+
+MANGLED = {"intersect_triangle3": "_Z19intersect_triangle3PdS_S_S_S_S_S_S_",
+           "triBoxOverlap": "_Z13triBoxOverlapPfS_PA3_f"}
+
+
+def test_cxx_linkage_symbols_exported():
+    """VRT/raytri.h:5-7 and VRT/tribox2.h:6 declare the primitives with C++
+    linkage, so VRT/voxel_octree.cc:446,490 import the mangled names; the
+    library exports both those and the C names of vrt.h."""
+    out = os.popen(f"nm -D --defined-only {vrt.LIB_PATH}").read().split()
+    for c_name, cxx_name in MANGLED.items():
+        assert c_name in out and cxx_name in out, (c_name, cxx_name)
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_reference_declared_caller_links_and_matches_kat(tmp_path):
+    """A C++ caller declaring the two functions exactly as the reference's
+    headers do (tests/legacy_link.cpp) links against libvrt.so alone and
+    reproduces the reference-generated KATs bit for bit."""
+    libdir = os.path.dirname(vrt.LIB_PATH)
+    exe = str(tmp_path / "legacy_link")
+    subprocess.run(["g++", "-O2", "-std=c++17", os.path.join(ROOT, "tests", "legacy_link.cpp"),
+                    "-o", exe, f"-L{libdir}", "-lvrt", f"-Wl,-rpath,{libdir}",
+                    "-Wl,-rpath-link,/opt/rocm/lib", "-Wl,--no-as-needed"], check=True)
+    nm = subprocess.run(["nm", "-u", exe], capture_output=True, text=True, check=True).stdout
+    assert all(m in nm for m in MANGLED.values()), nm
+    mt, sat = golden("kat_raytri.npz"), golden("kat_tribox.npz")
+    inp = (np.uint32(len(mt["inp"])).tobytes() + np.ascontiguousarray(mt["inp"], np.float64).tobytes()
+           + np.uint32(len(sat["inp"])).tobytes() + np.ascontiguousarray(sat["inp"], np.float32).tobytes())
+    env = dict(os.environ)
+    env["LD_LIBRARY_PATH"] = ":".join(p for p in (env.get("LD_LIBRARY_PATH", ""), "/opt/rocm/lib") if p)
+    res = subprocess.run([exe], input=inp, capture_output=True, env=env, timeout=120)
+    assert res.returncode == 0, res.stderr.decode()
+    n4 = len(mt["inp"]) * 4
+    got_mt = np.frombuffer(res.stdout[:n4 * 8], np.float64).reshape(-1, 4)
+    got_sat = np.frombuffer(res.stdout[n4 * 8:], np.int32)
+    np.testing.assert_array_equal(got_mt.view(np.uint64), mt["out"].view(np.uint64))
+    np.testing.assert_array_equal(got_sat, sat["out"])
