@@ -254,6 +254,17 @@ int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
  * soon as one of them has ended (every resume round but the last likewise),
  * so that nearly every secondary ray is saved and resumed at least once. */
 #define VRT_TEST_SPILL_ALL 4
+/* VRT_TEST_VIRTUAL_RANKS_N(n) (2 <= n <= 16), read by vrt_scene_create_multi:
+ * a one-device mask creates n *virtual* ranks on that device -- n scene
+ * replicas, n streams, the same per-rank send buffers, gather buffer, tile
+ * deal and unpack as n devices -- with the RCCL gather replaced by
+ * device-to-device copies of each rank's buffer into its slot of rank 0's
+ * receive buffer (ordered like the collective: after the rank's render on
+ * its stream, before rank 0's unpack).  RCCL refuses duplicate devices; this
+ * runs the n-rank frame on a one-GPU box.  Handles created without it are
+ * unaffected. */
+#define VRT_TEST_VIRTUAL_RANKS 8
+#define VRT_TEST_VIRTUAL_RANKS_N(n) (VRT_TEST_VIRTUAL_RANKS | ((n) << 8))
 int vrt_set_test_flags(int flags);
 
 /* Diagnostic: the records appended to each compaction queue (phase A, then

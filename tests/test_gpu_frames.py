@@ -417,3 +417,75 @@ def test_multi_device_frame_one_device_matches_oracle(proxy, nx, ny, depth):
             assert np.array_equal(bits(img.cpu().numpy()), bits(want)), pose
     finally:
         m.close()
+
+
+_MULTI_WANT = {}
+
+
+def _multi_want(proxy, depth, nx, ny, pose):
+    key = (depth, nx, ny, pose)
+    if key not in _MULTI_WANT:
+        tree, osc = scenes(proxy, depth)
+        mn, mx = tree.root_box
+        p = vrt.sweep_pose(mn, mx, pose, 16)
+        _MULTI_WANT[key] = osc.render(po.camera(*p), 1.0, 1.0, nx, ny, nthreads=NTH, samples=False)
+    return _MULTI_WANT[key]
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_multi_device_frame_virtual_ranks_match_oracle(proxy, nranks):
+    """The n > 1 branch of vrt_render_multi / vrt_render_multi_device
+    (per-rank send buffers, rank-major receive buffer, n-rank unpack) run on
+    one GPU with VRT_TEST_VIRTUAL_RANKS: n replicas on device 0, the gather
+    done by device copies ordered like the collective.  Film sizes change
+    204x122 -> 1920x1080 (buffers regrow) -> 204x122, through the host entry
+    point, then three frames queued on one stream without a host sync (each
+    rank's send buffer reused while rank 0 unpacks the previous frame)."""
+    import torch
+    depth = 8
+    m = vrt.MultiOctree(proxy, depth, device_mask=1, virtual_ranks=nranks)
+    try:
+        assert m.devices == [0] * nranks
+        mn, mx = m.root_box
+        seq = [(204, 122, 4), (1920, 1080, 10), (204, 122, 7)]
+        for nx, ny, pose in seq:
+            got = m.render(vrt.Camera(*vrt.sweep_pose(mn, mx, pose, 16)), vrt.Film(1, 1, nx, ny))
+            assert np.array_equal(bits(got), bits(_multi_want(proxy, depth, nx, ny, pose))), (nx, ny, pose)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        imgs = []
+        for nx, ny, pose in [(1920, 1080, 10), (204, 122, 4), (1920, 1080, 3)]:
+            img = torch.full((ny, nx, 3), 7.0, dtype=torch.float32, device="cuda:0")
+            m.render_device(vrt.Camera(*vrt.sweep_pose(mn, mx, pose, 16)), vrt.Film(1, 1, nx, ny),
+                            img.data_ptr(), s.cuda_stream)
+            imgs.append((img, nx, ny, pose))
+        s.synchronize()
+        for img, nx, ny, pose in imgs:
+            assert np.array_equal(bits(img.cpu().numpy()), bits(_multi_want(proxy, depth, nx, ny, pose))), \
+                (nx, ny, pose)
+    finally:
+        m.close()
+
+
+def test_multi_device_frame_two_devices_matches_oracle(proxy):
+    """A real 2-device frame (device_mask 0b11: a 2-rank RCCL communicator,
+    ncclGather across devices).  Skipped on a one-GPU box."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("fewer than 2 devices visible")
+    depth = 8
+    m = vrt.MultiOctree(proxy, depth, device_mask=0b11)
+    try:
+        assert m.devices == [0, 1]
+        mn, mx = m.root_box
+        for nx, ny, pose in [(1920, 1080, 10), (204, 122, 4)]:
+            cam, film = vrt.Camera(*vrt.sweep_pose(mn, mx, pose, 16)), vrt.Film(1, 1, nx, ny)
+            want = _multi_want(proxy, depth, nx, ny, pose)
+            assert np.array_equal(bits(m.render(cam, film)), bits(want)), (nx, ny, pose)
+            img = torch.full((ny, nx, 3), 7.0, dtype=torch.float32, device="cuda:0")
+            s = torch.cuda.Stream(device="cuda:0")
+            m.render_device(cam, film, img.data_ptr(), s.cuda_stream)
+            s.synchronize()
+            assert np.array_equal(bits(img.cpu().numpy()), bits(want)), (nx, ny, pose)
+    finally:
+        m.close()

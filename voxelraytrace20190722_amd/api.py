@@ -477,13 +477,23 @@ class MultiOctree:
     device's share of the tile deal + one ncclGather to the first device +
     unpack there -- render_mt (VRT/camera.h:42-68) over a node's GPUs."""
 
-    def __init__(self, scene, max_depth, device_mask=1, build_on_device=False):
+    def __init__(self, scene, max_depth, device_mask=1, build_on_device=False, virtual_ranks=None):
+        """virtual_ranks=n (test hook, VRT_TEST_VIRTUAL_RANKS_N): n ranks on
+        the one device of device_mask, the RCCL gather replaced by
+        device-to-device copies -- the n-rank frame on a one-GPU box."""
         self.scene = scene
         h = C.c_void_p()
         d = scene.desc()
         flags = _ffi.VRT_BUILD_DEVICE if build_on_device else 0
-        check(lib().vrt_scene_create_multi(C.byref(d), int(max_depth), int(device_mask), flags, C.byref(h)),
-              "vrt_scene_create_multi")
+        if virtual_ranks:
+            lib().vrt_set_test_flags(TEST_VIRTUAL_RANKS | (int(virtual_ranks) << 8))
+            try:
+                rc = lib().vrt_scene_create_multi(C.byref(d), int(max_depth), int(device_mask), flags, C.byref(h))
+            finally:
+                lib().vrt_set_test_flags(0)
+        else:
+            rc = lib().vrt_scene_create_multi(C.byref(d), int(max_depth), int(device_mask), flags, C.byref(h))
+        check(rc, "vrt_scene_create_multi")
         self.h = h
         n = C.c_int32()
         check(lib().vrt_multi_devices(self.h, C.byref(n), None), "vrt_multi_devices")
@@ -678,6 +688,7 @@ def build_id():
 TEST_FORCE_DEFER = 1  # include/vrt.h VRT_TEST_FORCE_DEFER
 TEST_FAIL_LAUNCH = 2  # include/vrt.h VRT_TEST_FAIL_LAUNCH
 TEST_SPILL_ALL = 4  # include/vrt.h VRT_TEST_SPILL_ALL
+TEST_VIRTUAL_RANKS = 8  # include/vrt.h VRT_TEST_VIRTUAL_RANKS (count << 8)
 
 
 def set_test_flags(flags):

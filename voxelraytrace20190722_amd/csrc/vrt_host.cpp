@@ -1190,6 +1190,8 @@ extern "C" int vrt_set_test_flags(int flags)
         return VRT_OK;
 }
 
+int vrt::test_flags() { return g_test_flags.load(); }
+
 static void fill_render_params(vrt_scene *s, const vrt_camera *cam,
                                const vrt_film *film, int rank, int nranks,
                                RenderParams *p)

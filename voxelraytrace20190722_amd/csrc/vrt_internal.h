@@ -476,6 +476,8 @@ hipError_t build_tree_device(int device, const float *pos, int ntri, const float
 int scene_replicate(const vrt_scene *src, const vrt_scene_desc *d, int device, vrt_scene **out);
 // memcpy of a large host range over up to 4 threads.
 void par_memcpy(void *dst, const void *src, size_t bytes);
+// the process-wide vrt_set_test_flags value
+int test_flags();
 
 // Kernel launchers (vrt_kernels.hip)
 // Which primary-render kernel launch_render runs: the one-wave grid

@@ -27,7 +27,8 @@ using namespace vrt;
 struct vrt_multi {
         std::vector<int> devs;          // rank i -> HIP device
         std::vector<vrt_scene *> sc;    // rank i's replica of the scene
-        std::vector<ncclComm_t> comm;   // ncclCommInitAll over devs
+        std::vector<ncclComm_t> comm;   // ncclCommInitAll over devs (empty: virtual ranks)
+        bool virt = false;              // VRT_TEST_VIRTUAL_RANKS: n ranks on one device, copies for the gather
         std::vector<hipStream_t> st;    // rank i's render + collective stream
         std::vector<hipEvent_t> ev;     // rank i: its part of a frame queued
         std::vector<float *> send;      // ranks >= 1: packed tile buffer (tpr * 192 floats)
@@ -102,6 +103,45 @@ int sync_all(vrt_multi *m)
         return VRT_OK;
 }
 
+// The ranks' packed buffers into rank 0's receive buffer m->gath (rank-major,
+// `count` floats each), after each rank's render on its stream; rank 0's
+// stream then holds the complete buffer.
+int gather(vrt_multi *m, size_t count)
+{
+        const int n = (int)m->devs.size();
+        if (m->virt) {
+                // VRT_TEST_VIRTUAL_RANKS: rank i's buffer into its slot on rank
+                // i's stream (after its render, where the collective's send
+                // runs), and -- as the collective waits for the root -- only
+                // once rank 0's stream has reached this frame's gather (so the
+                // previous frame's unpack has read the slot); rank 0's stream
+                // then waits for every copy
+                HIPCHK(hipSetDevice(m->devs[0]));
+                HIPCHK(hipEventRecord(m->ev[0], m->st[0]));
+                for (int i = 1; i < n; ++i)
+                        HIPCHK(hipStreamWaitEvent(m->st[i], m->ev[0], 0));
+                for (int i = 1; i < n; ++i) {
+                        HIPCHK(hipMemcpyAsync(m->gath + (size_t)i * count, m->send[i], count * sizeof(float),
+                                              hipMemcpyDeviceToDevice, m->st[i]));
+                        HIPCHK(hipEventRecord(m->ev[i], m->st[i]));
+                        HIPCHK(hipStreamWaitEvent(m->st[0], m->ev[i], 0));
+                }
+                return VRT_OK;
+        }
+        // one RCCL gather to rank 0 (in place for rank 0: sendbuff == recvbuff + 0)
+        NCCLCHK(ncclGroupStart());
+        for (int i = 0; i < n; ++i) {
+                const ncclResult_t r = ncclGather(i == 0 ? m->gath : m->send[i], i == 0 ? m->gath : nullptr, count,
+                                                  ncclFloat32, 0, m->comm[i], m->st[i]);
+                if (r != ncclSuccess) {
+                        (void)ncclGroupEnd();
+                        return set_error(VRT_E_DEVICE, "ncclGather (rank %d): %s", i, ncclGetErrorString(r));
+                }
+        }
+        NCCLCHK(ncclGroupEnd());
+        return VRT_OK;
+}
+
 // One frame into d_image on rank 0's device (caller holds m->mu).
 int render_multi(vrt_multi *m, const vrt_camera *cam, const vrt_film *film, float *d_image, hipStream_t caller)
 {
@@ -132,17 +172,8 @@ int render_multi(vrt_multi *m, const vrt_camera *cam, const vrt_film *film, floa
                         if (int rc = vrt_render_tiles_device(m->sc[i], cam, film, i, n, 0, dst, m->st[i]))
                                 return rc;
                 }
-                // one gather to rank 0 (in place for rank 0: sendbuff == recvbuff + 0)
-                NCCLCHK(ncclGroupStart());
-                for (int i = 0; i < n; ++i) {
-                        const ncclResult_t r = ncclGather(i == 0 ? m->gath : m->send[i], i == 0 ? m->gath : nullptr,
-                                                          count, ncclFloat32, 0, m->comm[i], m->st[i]);
-                        if (r != ncclSuccess) {
-                                (void)ncclGroupEnd();
-                                return set_error(VRT_E_DEVICE, "ncclGather (rank %d): %s", i, ncclGetErrorString(r));
-                        }
-                }
-                NCCLCHK(ncclGroupEnd());
+                if (int rc = gather(m, count))
+                        return rc;
         }
         HIPCHK(hipSetDevice(m->devs[0]));
         if (tpr > 0) {
@@ -197,9 +228,17 @@ extern "C" int vrt_scene_create_multi(const vrt_scene_desc *desc, int max_depth,
         if (!out)
                 return set_error(VRT_E_INVALID, "null out");
         *out = nullptr;
-        const std::vector<int> devs = mask_devices(device_mask);
+        std::vector<int> devs = mask_devices(device_mask);
         if (devs.empty())
                 return set_error(VRT_E_INVALID, "empty device mask");
+        const int tf = test_flags();
+        const bool virt = (tf & VRT_TEST_VIRTUAL_RANKS) != 0;
+        if (virt) {
+                const int nv = (tf >> 8) & 0xff;
+                if (devs.size() != 1 || nv < 2 || nv > 16)
+                        return set_error(VRT_E_INVALID, "virtual ranks need a one-device mask and 2..16 ranks (got %d)", nv);
+                devs.assign(nv, devs[0]);
+        }
         int nvis = 0;
         if (hipGetDeviceCount(&nvis) != hipSuccess || devs.back() >= nvis)
                 return set_error(VRT_E_NODEVICE, "device mask %#x names device %d, %d visible", device_mask,
@@ -241,8 +280,11 @@ extern "C" int vrt_scene_create_multi(const vrt_scene_desc *desc, int max_depth,
         }
         HIPCHK(hipSetDevice(devs[0]));
         HIPCHK(hipEventCreateWithFlags(&m->ev_in, hipEventDisableTiming));
-        m->comm.assign(n, nullptr);
-        NCCLCHK(ncclCommInitAll(m->comm.data(), n, m->devs.data()));
+        m->virt = virt;
+        if (!virt) {
+                m->comm.assign(n, nullptr);
+                NCCLCHK(ncclCommInitAll(m->comm.data(), n, m->devs.data()));
+        }
         *out = m.release();
         return VRT_OK;
 }
