@@ -148,6 +148,12 @@ int vrt_make_ray(const float o[3], const float d[3], float tmin, float tmax,
                  vrt_ray *out);
 /* AABB3D::isect(ray, nullptr) on the host (box = min xyz, max xyz). */
 int vrt_aabb_isect(const float box[6], const vrt_ray *ray);
+/* *bound = an upper bound on the gen_rays4 rays of the film with a direction
+ * component |d_q| < 2^-64 (an exact zero included): the rays the fast-only
+ * persistent render defers to its exact pass.  0 certifies that the frame
+ * needs no deferred pass (it is then not launched); INT64_MAX when a camera
+ * term is not finite.  Never below the true count. */
+int vrt_camera_defer_bound(const vrt_camera *cam, const vrt_film *film, int64_t *bound);
 
 /* ---- the hot path ------------------------------------------------------ */
 /* Primary render = the per-pixel loop of VRT/main.cc:118-123 with the

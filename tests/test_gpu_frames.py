@@ -222,6 +222,36 @@ def test_forced_defer_pass_matches_oracle(proxy):
         assert np.array_equal(bits(got), bits(want))
 
 
+def test_naturally_deferred_rays_match_oracle(proxy):
+    """Rays with an exactly zero direction component (the reference's FLT_MIN
+    substitution, outside the fast-only kernel's finite-slab contract) are
+    deferred and rendered by k_render_defer on a grid sized by the host's
+    bound (vrt_camera_defer_bound), without any test flag: a camera built so
+    that d_y cancels on a line of sample-1 rays (nx = 5 ny), and the sweep
+    pose whose 1080p frame holds one such ray.  A frame with bound 0 runs
+    without the deferred pass; all are bit-exact."""
+    tree, osc = scenes(proxy, 8)
+    mn, mx = tree.root_box
+    fov, eye, spot, up = vrt.sweep_pose(mn, mx, 5, 16)
+    cam = vrt.Camera(fov, eye, spot, up)
+    ocam = po.camera(fov, eye, spot, up)
+    for k, v in ((1, 0.5), (5, 0.5), (9, 0.0)):  # s.y = u.y = 0.5, nf.y = 0
+        cam.c.C[k] = v
+        ocam[k] = v
+    for nx, ny in ((400, 80), (1280, 256)):
+        f = vrt.Film(1, 1, nx, ny)
+        assert cam.defer_bound(f) > 0
+        want = osc.render(ocam, 1.0, 1.0, nx, ny, nthreads=NTH, samples=False)
+        got = _device_image(tree, cam, f)
+        assert np.array_equal(bits(got), bits(want)), (nx, ny)
+    bounds = [vrt.Camera(*vrt.sweep_pose(mn, mx, k, 16)).defer_bound(vrt.Film(1, 1, 1920, 1080)) for k in range(16)]
+    for pose in (int(np.argmax(bounds)), int(np.argmin(bounds))):
+        p = vrt.sweep_pose(mn, mx, pose, 16)
+        want = osc.render(po.camera(*p), 1.0, 1.0, 1920, 1080, nthreads=NTH, samples=False)
+        got = _device_image(tree, vrt.Camera(*p), vrt.Film(1, 1, 1920, 1080))
+        assert np.array_equal(bits(got), bits(want)), (pose, bounds[pose])
+
+
 def _frame_ms(tree, cam, film, img, n):
     """Mean device time of n production launches into img (HIP events)."""
     import torch

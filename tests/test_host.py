@@ -382,3 +382,48 @@ def test_multi_device_create_rejects_bad_masks():
     with pytest.raises(vrt.VrtError) as e:  # device 31 is never visible (none here)
         vrt.MultiOctree(sd, 3, device_mask=1 << 31)
     assert e.value.status == _ffi.VRT_E_NODEVICE
+
+
+def _deferring_rays(cam, film):
+    """Brute force: the gen_rays4 rays of the film with a direction component
+    |d| < 2^-64 (zero included) -- the rays the fast-only render defers
+    (fin_ok, vrt_kernels.hip)."""
+    n = 0
+    for py in range(film.ny):
+        for px in range(film.nx):
+            d = cam.gen_rays4(film, px, py)[:, 3:6]  # rows: o xyz, d xyz, tmin, tmax
+            n += int((np.abs(d) < np.float32(2.0 ** -64)).any(axis=1).sum())
+    return n
+
+
+def adversarial_camera():
+    """A camera whose y direction component cancels exactly: s_y = u_y = 0.5,
+    nf_y = 0, so d_y = 0.5 x_ + 0.5 y_ = 0 where (x + sx)/nx = -(y + sy)/ny;
+    with nx = 5 ny, sample 1 (sx, sy) = (3/8, 1/8) hits it on x + 5y = -1."""
+    cam = vrt.Camera(vrt.to_radian(70), (0.3, 0.6, -2.0), (0.1, 0.5, 0.0), (0.0, 1.0, 0.0))
+    cam.c.C[1] = 0.5   # s.y
+    cam.c.C[5] = 0.5   # u.y
+    cam.c.C[9] = 0.0   # nf.y
+    return cam
+
+
+def test_camera_defer_bound_is_an_upper_bound():
+    """vrt_camera_defer_bound (the host bound that lets a frame skip the
+    deferred pass, or size its grid) is never below the brute-force count of
+    deferring rays, is 0 for ordinary cameras, and tight on the sweep."""
+    films = [vrt.Film(1, 1, 64, 48), vrt.Film(1, 1, 33, 17), vrt.Film(1, 1, 80, 16)]
+    for ci in range(len(CAMS)):
+        cam = vrt.Camera(*CAMS[ci])
+        for f in films:
+            assert cam.defer_bound(f) >= _deferring_rays(cam, f)
+    cam = adversarial_camera()
+    f = vrt.Film(1, 1, 80, 16)
+    n = _deferring_rays(cam, f)
+    assert n > 0 and cam.defer_bound(f) >= n
+    # a real sweep: near-cancellations exist, exact zeros at some poses
+    mn, mx = np.array([-1, 0, -1], np.float32), np.array([1, 1, 1], np.float32)
+    bounds = [vrt.Camera(*vrt.sweep_pose(mn, mx, k, 16)).defer_bound(vrt.Film(1, 1, 320, 180)) for k in range(16)]
+    for k in (0, 1, 5):
+        cam = vrt.Camera(*vrt.sweep_pose(mn, mx, k, 16))
+        assert bounds[k] >= _deferring_rays(cam, vrt.Film(1, 1, 320, 180))
+    assert max(bounds) < 64

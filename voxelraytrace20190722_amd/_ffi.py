@@ -122,6 +122,7 @@ SIGNATURES = {
     "stbi_write_hdr": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, f32p]),
     "vrt_build_id": (C.c_char_p, []),
     "vrt_set_test_flags": (C.c_int, [C.c_int]),
+    "vrt_camera_defer_bound": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]),
     "vrt_secondary_spill_counts": (C.c_int, [_P, i64p]),
     "vrt_device_selftest_order": (C.c_int, [C.c_int, f32p, u32p, C.c_int64, u32p, f32p, i32p, C.c_int64,
                                             C.c_int32, i32p]),

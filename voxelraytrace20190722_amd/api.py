@@ -65,6 +65,13 @@ class Camera:
               "vrt_gen_rays4")
         return self._rays(arr)
 
+    def defer_bound(self, film):
+        """vrt_camera_defer_bound: an upper bound on the rays of the film the
+        fast-only render defers (0: no deferred pass is launched)."""
+        n = C.c_int64()
+        check(lib().vrt_camera_defer_bound(C.byref(self.c), C.byref(film.c), C.byref(n)), "vrt_camera_defer_bound")
+        return n.value
+
     def gen_rays1(self, film, px, py):
         arr = (_ffi.Ray * 1)()
         check(lib().vrt_gen_rays1(C.byref(self.c), C.byref(film.c), int(px), int(py), arr),

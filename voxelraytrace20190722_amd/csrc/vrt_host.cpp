@@ -191,6 +191,16 @@ static int gen_rays(const vrt_camera *cam, const vrt_film *film, int px,
         return VRT_OK;
 }
 
+extern "C" int vrt_camera_defer_bound(const vrt_camera *cam, const vrt_film *film, int64_t *bound)
+{
+        if (!cam || !film || !bound || film->nx < 1 || film->ny < 1)
+                return fail(VRT_E_INVALID, "vrt_camera_defer_bound: bad argument");
+        CamParams cp;
+        fill_cam_params(cam, film, &cp);
+        *bound = camera_defer_bound(cp);
+        return VRT_OK;
+}
+
 extern "C" int vrt_gen_rays4(const vrt_camera *cam, const vrt_film *film,
                              int px, int py, vrt_ray out[4])
 {

@@ -487,6 +487,9 @@ int test_flags();
 // persistent kinds take their units from p.q.
 enum RenderKind { kRenderGrid = 0, kRenderPersist = 1, kRenderPersistFast = 2 };
 RenderKind render_kind(const RenderParams &p, bool instrumented);
+// upper bound on the camera rays of the film that fail the fast-only
+// kernel's per-wave check (vrt_kernels.hip; cached for the last 32 cameras)
+int64_t camera_defer_bound(const CamParams &c);
 // *q_waves = the failing adds each slice counter receives (the waves
 // launched that visit it), slice_units[x] = the units of slice x (all 0 when
 // no work queue was used), for the queue bases

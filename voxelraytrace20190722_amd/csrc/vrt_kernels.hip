@@ -27,6 +27,8 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 namespace vrt {
 
@@ -2501,6 +2503,116 @@ RenderKind render_kind(const RenderParams &p, bool instrumented)
         return fast ? kRenderPersistFast : kRenderPersist;
 }
 
+// Host bound on the camera rays of a frame that make k_render_p<true> defer
+// their unit (so the deferred pass is launched only for frames that have
+// some, on a grid sized to them).  Every ray has tmin = +0, tmax = FLT_MAX
+// and a finite origin (render_kind); it defers iff a direction component
+// fails fin_ok / fast_ok, i.e. |d_q| < 2^-64 (an exact zero included).
+// d = normalize(acc) with acc_q = fl(fl(a + b) + c), a = fl(s_q x_) over the
+// film's columns, b = fl(u_q y_) over its rows, c = fl(nf_q z) (+ e_q * 0,
+// which adds a zero: camera_dir).  The two float additions are off from the
+// real a + b + c by at most 2.01 * 2^-24 * M_q (M_q >= |a| + |b| + |c|,
+// + 2^-140 for subnormals).  For every row b the distinct a values within
+// that bound + T (T = 2^-58 * M, M = sum of the M_q >= len) of -(b + c) are
+// found by binary search and their float sum is evaluated exactly as the
+// kernel does; a sum of at most 2^-62 * M counts the columns holding that a
+// value.  Every other ray has |acc_q| > 2^-62 * M, so |d_q| = |acc_q| / len
+// > 2^-62 / 1.01 > 2^-64.  The count is an upper bound (a ray may count for
+// two components); a non-finite term returns INT64_MAX.  On the 16-pose
+// 1080p sweep about half the poses have a ray or two with an exactly zero
+// component.  Cost: O(ny log nx) per sample and component; the last 32
+// cameras' answers are kept (a camera sweep repeats its poses).
+static int64_t camera_defer_count(const CamParams &c);
+int64_t camera_defer_bound(const CamParams &c)
+{
+        struct Entry {
+                CamParams c;
+                int64_t n;
+        };
+        static std::mutex mu;
+        static Entry cache[32];
+        static int n = 0, next = 0;
+        {
+                std::lock_guard<std::mutex> lk(mu);
+                for (int i = 0; i < n; ++i)
+                        if (std::memcmp(&cache[i].c, &c, sizeof c) == 0)
+                                return cache[i].n;
+        }
+        const int64_t r = camera_defer_count(c);
+        std::lock_guard<std::mutex> lk(mu);
+        cache[next] = Entry{ c, r };
+        next = (next + 1) % 32;
+        n = std::min(n + 1, 32);
+        return r;
+}
+
+static int64_t camera_defer_count(const CamParams &c)
+{
+        const int nx = c.nx, ny = c.ny;
+        if (nx < 1 || ny < 1)
+                return 0;
+        std::vector<float> xs((size_t)nx), ys((size_t)ny), a, b((size_t)ny);
+        std::vector<int> mult;
+        a.reserve((size_t)nx);
+        int64_t count = 0;
+        for (int s = 0; s < 4; ++s) {
+                const float sx = sample_x(s), sy = sample_y(s);
+                // the same float ops as camera_dir
+                for (int px = 0; px < nx; ++px)
+                        xs[px] = ((float)(px - nx / 2) + sx) / (float)nx;
+                for (int py = 0; py < ny; ++py)
+                        ys[py] = ((float)((ny - 1 - py) - ny / 2) + sy) / (float)ny;
+                double m[3], mtot = 0.0;
+                for (int q = 0; q < 3; ++q) {
+                        const double ax = std::max(std::fabs((double)(c.s[q] * xs[0])),
+                                                   std::fabs((double)(c.s[q] * xs[nx - 1])));
+                        const double by = std::max(std::fabs((double)(c.u[q] * ys[0])),
+                                                   std::fabs((double)(c.u[q] * ys[ny - 1])));
+                        m[q] = ax + by + std::fabs((double)(c.nf[q] * c.z));
+                        if (!std::isfinite(m[q]) || !std::isfinite((double)c.e[q]) || m[q] > 0x1p100)
+                                return INT64_MAX;
+                        mtot += m[q];
+                }
+                const double T = 0x1p-58 * mtot;                  // beyond the window: |acc_q| > T
+                const float exact_min = (float)(0x1p-62 * mtot);  // inside it: the float sum itself
+                for (int q = 0; q < 3; ++q) {
+                        const float sq = c.s[q], uq = c.u[q], cq = c.nf[q] * c.z;
+                        // the distinct a values, ascending, with their column counts
+                        a.clear();
+                        for (int px = 0; px < nx; ++px)
+                                a.push_back(sq * xs[px]);
+                        std::sort(a.begin(), a.end());
+                        mult.clear();
+                        size_t w = 0;
+                        for (size_t i = 0; i < a.size(); ++i) {
+                                if (w > 0 && a[i] == a[w - 1]) {
+                                        ++mult[w - 1];
+                                } else {
+                                        a[w++] = a[i];
+                                        mult.push_back(1);
+                                }
+                        }
+                        a.resize(w);
+                        for (int py = 0; py < ny; ++py)
+                                b[py] = uq * ys[py];
+                        const double err = 2.01 * 0x1p-24 * m[q] + 0x1p-140 + T;
+                        for (int py = 0; py < ny; ++py) {
+                                const double t = -((double)b[py] + (double)cq);
+                                size_t i = std::lower_bound(a.begin(), a.end(), (float)(t - err * 1.001)) - a.begin();
+                                for (; i < a.size() && (double)a[i] <= t + err * 1.001; ++i) {
+                                        // a near-cancellation: camera_dir's own float sum
+                                        float acc = a[i];
+                                        acc += b[py];
+                                        acc += cq;
+                                        if (!(std::fabs(acc) > exact_min))
+                                                count += mult[i];
+                                }
+                        }
+                }
+        }
+        return count;
+}
+
 bool secondary_uses_queue(const DevScene &sc)
 {
         return VRT_SEC_PERSIST && sc.sec_blocks > 0;
@@ -2568,8 +2680,18 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                                 return e;
                         if (p.test_flags & VRT_TEST_FAIL_LAUNCH)  // test hook: fail between the two launches
                                 return hipErrorLaunchFailure;
-                        hipLaunchKernelGGL(k_render_defer, dim3(std::max(8, (g / 2) & ~7)), dim3(kPersistBlock), 0,
-                                           st, p);
+                        // the deferred pass only when some ray of the frame may
+                        // defer, on half the persistent grid, or fewer blocks when
+                        // the host's bound says only a few units can be deferred
+                        // (each of the grid's waves then takes at most one)
+                        const int64_t nd = (p.test_flags & VRT_TEST_FORCE_DEFER) ? INT64_MAX
+                                                                                  : camera_defer_bound(p.cam);
+                        if (nd > 0) {
+                                const int half = std::max(8, (g / 2) & ~7);
+                                const int64_t want = ((nd + 3) / 4 + 7) & ~int64_t(7);
+                                const int gd = (int)std::min<int64_t>(half, std::max<int64_t>(8, want));
+                                hipLaunchKernelGGL(k_render_defer, dim3(gd), dim3(kPersistBlock), 0, st, p);
+                        }
                 } else {
                         hipLaunchKernelGGL(k_render_p<false>, dim3(g), dim3(kPersistBlock), 0, st, p);
                 }
