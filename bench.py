@@ -322,6 +322,34 @@ def nccl_options():
         return None
 
 
+def ranks_seen(backend, dev):
+    """ranks counted by an all_reduce over the process group"""
+    t = torch.ones(1, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t)
+    return int(t.item())
+
+
+RANK_FIELDS = ("share_render_ms", "collective_ms", "unpack_ms", "elapsed_s")
+
+
+def per_rank_report(world, backend, dev, rank, vals):
+    """Every rank's diagnostic numbers (RANK_FIELDS) gathered to every rank
+    (all_gather: each rank calls) -> the per-rank list rank 0 prints.  share:
+    the mean render span of this rank's share (HIP events on its stream);
+    collective: from the end of the render to the frame's gather / reduce
+    being complete on the stream that waits for it; unpack: rank 0's
+    re-assembly kernel (0 elsewhere)."""
+    t = torch.tensor([float(rank)] + [float(v) for v in vals], dtype=torch.float64,
+                     device=dev if backend == "nccl" else "cpu")
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    rows = []
+    for o in out:
+        v = o.tolist()
+        rows.append({"rank": int(v[0]), **{k: round(x, 4) for k, x in zip(RANK_FIELDS, v[1:])}})
+    return rows
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -371,6 +399,13 @@ def parse():
                         "tiles as one of R ranks, RCCL gather over a 1-rank process group, unpack of R rank "
                         "buffers -- the per-rank GPU and host cost of the multi-GPU step without the xGMI "
                         "transfer (reported as 'rehearsal', never as the N-GPU value)")
+    p.add_argument("--abi-multi", action="store_true",
+                   help="one process over every visible GPU through the library's own multi-device frame "
+                        "(vrt_scene_create_multi + vrt_render_multi_device: scene per device, RCCL gather, "
+                        "unpack on device 0) -- the C++ caller's render_mt replacement (primary mode)")
+    p.add_argument("--abi-multi-virtual", type=int, default=0,
+                   help="with --abi-multi on one GPU: N virtual ranks (VRT_TEST_VIRTUAL_RANKS: the N-rank "
+                        "path with device copies in place of the gather), reported as a rehearsal")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher check only: form the process group (gloo), count the ranks, print one line; "
                         "no GPU is used")
@@ -420,8 +455,80 @@ def spawn_ranks(n):
     return rc
 
 
+def abi_multi(a):
+    """--abi-multi: the library's own multi-device frame in ONE process over
+    every visible GPU (vrt_scene_create_multi: the octree built once and
+    uploaded per device, one RCCL communicator; vrt_render_multi_device per
+    frame: every device's share of the tile deal, ncclGather to device 0,
+    unpack there) -- what a C++ caller of render_mt's replacement gets.  K
+    frames of the sweep queued on one stream of device 0 (wall clock around
+    them, then a sync); the last frame is compared bit for bit with the
+    single-device render of the same pose.  --abi-multi-virtual N on one GPU:
+    N virtual ranks (device copies in place of the gather), a rehearsal."""
+    ndev = torch.cuda.device_count()
+    virt = a.abi_multi_virtual if a.abi_multi_virtual > 1 else 0
+    n = virt or ndev
+    mask = 1 if virt else (1 << ndev) - 1
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    sd = vrt.obj2voxel(a.scene) if a.scene else vrt.SceneData.proxy(a.detail, 1)
+    t0 = time.time()
+    m = vrt.MultiOctree(sd, a.depth, device_mask=mask, virtual_ranks=virt or None)
+    log(f"[abi-multi] {n} ranks on devices {m.devices}: scene replicated + communicator in {time.time() - t0:.1f} s")
+    mn, mx = m.root_box
+    cams = [vrt.Camera(*vrt.sweep_pose(mn, mx, i, a.poses)) for i in range(a.poses)]
+    film = vrt.Film(1.0, 1.0, a.width, a.height)
+    rays = 8 * (a.width // 8) * 8 * (a.height // 8) * 4
+    st = torch.cuda.Stream(dev)
+    imgs = [torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev) for _ in range(2)]
+    for k in range(a.warmup):
+        m.render_device(cams[k % a.poses], film, imgs[k % 2].data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t_start = time.perf_counter()
+    for k in range(a.steps):
+        ev[k][0].record(st)
+        m.render_device(cams[k % a.poses], film, imgs[k % 2].data_ptr(), st.cuda_stream)
+        ev[k][1].record(st)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    span = float(np.mean([x.elapsed_time(y) for x, y in ev]))
+    last = (a.steps - 1) % a.poses
+    tree = vrt.VoxelOctree(sd, a.depth, device=0)
+    ref = torch.zeros_like(imgs[0])
+    tree.render_tiles_device(cams[last], film, 0, 1, 1, ref.data_ptr(), None)
+    torch.cuda.synchronize()
+    same = bool(torch.equal(imgs[(a.steps - 1) % 2].view(torch.int32), ref.view(torch.int32)))
+    tree.close()
+    m.close()
+    if not same:
+        raise SystemExit("abi-multi: the multi-device frame differs from the single-device render")
+    value = rays * a.steps / elapsed / 1e6
+    out = {"metric": f"Mrays/s at {a.width}x{a.height} Sponza {int(round(2 ** a.depth))}^3 octree (primary rays, "
+                     f"4 spp), in-library multi-device frame",
+           "value": None if virt else round(value, 2), "unit": "Mrays/s", "n_gpus": 1 if virt else n,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32+f64",
+           "data": "synthetic: deterministic sponza-proxy atrium (sponza.obj absent), 16-pose camera sweep",
+           "config": {"workload": f"primary render {a.width}x{a.height} x4 spp, max_depth {a.depth}",
+                      "parallelism": (f"vrt_render_multi_device: {n} ranks, scene per device, "
+                                      + ("device copies for the gather (VRT_TEST_VIRTUAL_RANKS rehearsal on one GPU)"
+                                         if virt else "RCCL ncclGather to device 0 + unpack"))},
+           "abi_multi": {"ranks": n, "devices": mask, "virtual": bool(virt), "call_span_ms_mean": round(span, 4),
+                         "last_frame_bit_exact_vs_single_device": same},
+           "build_id": vrt.build_id()}
+    if virt:
+        out["metric"] = "rehearsal: " + out["metric"]
+        out["abi_multi"]["frames_per_s_one_gpu"] = round(a.steps / elapsed, 2)
+    print(json.dumps(out), flush=True)
+
+
 def main():
     a = parse()
+    if a.abi_multi:
+        if "WORLD_SIZE" in os.environ and os.environ["WORLD_SIZE"] != "1":
+            raise SystemExit("--abi-multi runs in one process over every visible GPU (no launcher)")
+        return abi_multi(a)
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         # never fall back silently to one rank: N GPUs means N rank processes
         sys.exit(spawn_ranks(a.gpus))
@@ -434,15 +541,18 @@ def main():
     if a.dry_run:
         # launcher check without a GPU: the process group forms and every
         # rank is counted (gloo on the host)
+        per_rank = None
         if world > 1:
             dist.init_process_group("gloo")
-            t = torch.ones(1)
-            dist.all_reduce(t)
-            seen = int(t.item())
+            seen = ranks_seen("gloo", None)
+            per_rank = per_rank_report(world, "gloo", None, rank, [0.0] * len(RANK_FIELDS))
         else:
             seen = 1
         if rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": a.gpus, "ranks_seen": seen}), flush=True)
+            line = {"dry_run": True, "n_gpus": a.gpus, "ranks_seen": seen}
+            if per_rank:
+                line["per_rank"] = per_rank
+            print(json.dumps(line), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -540,6 +650,13 @@ def main():
     works = [None] * nbuf
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(a.steps)]
+    # N-rank diagnostics per timed frame: the collective complete on the
+    # stream that waits for it, and rank 0's unpack span
+    frame_of = [None] * nbuf
+    ev_coll = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+    ev_unp = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(a.steps)]
+    coll_done, unp_done = [], []
     torch.cuda.synchronize()  # buffers were zeroed on torch's stream; frames run on several
 
     def sl(k):
@@ -553,13 +670,23 @@ def main():
         with torch.cuda.stream(s):
             works[b].wait()  # stream-wait on the collective, no host block
         works[b] = None
+        k = frame_of[b]
+        frame_of[b] = None
+        if k is not None:
+            ev_coll[k].record(s)
+            coll_done.append(k)
         if rank == 0:  # each buffer slot re-assembles into its own image (frames in flight)
+            if k is not None:
+                ev_unp[k][0].record(s)
             if secondary:
                 with torch.cuda.stream(s):
                     imgs[b % nfl].copy_(visb[b])
             else:
                 vrt.unpack_tiles_device(film, nshare, gathered[b].data_ptr(), imgs[b % nfl].data_ptr(),
                                         s.cuda_stream)
+            if k is not None:
+                ev_unp[k][1].record(s)
+                unp_done.append(k)
 
     def step_secondary(k, timed):
         cam = cams[k % a.poses]
@@ -586,6 +713,7 @@ def main():
         if a.dist_backend == "nccl":
             with torch.cuda.stream(s):
                 works[b] = dist.reduce(visb[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
+            frame_of[b] = k if timed else None
             jp, bp = sl(k - 1)
             finish(bp, streams[jp])  # frame k-1: its reduce overlapped this render
         else:
@@ -633,6 +761,7 @@ def main():
             # the next frame's render and runs beside it
             with torch.cuda.stream(s):
                 works[b] = dist.gather(tiles[b], gl[b], dst=0, async_op=True)
+            frame_of[b] = k if timed else None
             jp, bp = sl(k - 1)
             finish(bp, streams[jp])  # frame k-1: its gather overlapped this render
         else:  # gloo rehearsal (several ranks on one GPU): host-staged gather
@@ -666,11 +795,22 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    elapsed_local = elapsed
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kms = np.array([s.elapsed_time(e) for s, e in ev])  # render launch span (HIP events on its stream), ms
+    per_rank = None
+    if world > 1 or (rehearse and not a.rehearse_render_only):
+        coll_ms = float(np.mean([ev[k][1].elapsed_time(ev_coll[k]) for k in coll_done])) if coll_done else 0.0
+        unp_ms = float(np.mean([ev_unp[k][0].elapsed_time(ev_unp[k][1]) for k in unp_done])) if unp_done else 0.0
+        vals = [float(kms.mean()), coll_ms, unp_ms, elapsed_local]
+        if world > 1:
+            per_rank = per_rank_report(world, a.dist_backend, dev, rank, vals)
+            seen = ranks_seen(a.dist_backend, dev)
+        else:
+            per_rank = [{"rank": 0, **{k_: round(v_, 4) for k_, v_ in zip(RANK_FIELDS, vals)}}]
     # per-frame device time: the launch span with one frame in flight; with
     # several, spans overlap (a span also holds the wait for the CUs the
     # previous frame still occupies), so the frame time is the step time
@@ -994,7 +1134,8 @@ def main():
         value = total_rays / elapsed / 1e6
         out = {
             "metric": metric,
-            "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "ranks_seen": world, "steps": a.steps,
+            "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "ranks_seen": seen if world > 1 else 1,
+            "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32+f64",
             "data": data_desc + ", 16-pose camera sweep",
@@ -1012,6 +1153,8 @@ def main():
         }
         if secondary and trace_kernels:
             out["roofline_per_kernel"] = trace_kernels
+        if per_rank:
+            out["per_rank"] = per_rank
         if d9:
             out["depth_plus1"] = d9
         if host_out:

@@ -91,7 +91,9 @@ def test_partition_covers_every_tile_and_pixel_once():
 def test_bench_spawns_one_rank_per_gpu(n):
     """`python bench.py --gpus N` without a launcher starts N rank processes
     (never a silent 1-rank run): in --dry-run mode (gloo, no GPU) rank 0
-    reports N ranks seen by an all_reduce over the group."""
+    reports N ranks seen by an all_reduce over the group, and the per-rank
+    diagnostics (share render, collective wait, unpack, elapsed) of every
+    rank through the same all_gather an N-GPU line uses."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -100,7 +102,12 @@ def test_bench_spawns_one_rank_per_gpu(n):
                         "--dry-run"], env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert lines == [{"dry_run": True, "n_gpus": n, "ranks_seen": n}]
+    assert len(lines) == 1
+    ln = lines[0]
+    assert {k: ln[k] for k in ("dry_run", "n_gpus", "ranks_seen")} == {"dry_run": True, "n_gpus": n, "ranks_seen": n}
+    assert [r["rank"] for r in ln["per_rank"]] == list(range(n))
+    for r in ln["per_rank"]:
+        assert set(r) == {"rank", "share_render_ms", "collective_ms", "unpack_ms", "elapsed_s"}
 
 
 def test_bench_refuses_world_size_mismatch():

@@ -1352,7 +1352,7 @@ static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int ra
         if (secondary_uses_queue(p.sc)) {
                 if (int rc = queue_take(s, st, &q, &slot))
                         return rc;
-                if (!s_tri && !s_vox) {  // the occlusion walk: compaction
+                if (!VRT_SEC_COOP && !s_tri && !s_vox) {  // the occlusion walk: compaction
                         const int64_t rays = deal_count(tile_deal(p.ntx, p.nty, nranks), rank) * 64 * (int64_t)spp;
                         if (int rc = spill_setup(s, rays, st, &sq, &set))
                                 return rc;

@@ -41,6 +41,12 @@ static_assert(sizeof(XNodeRec) == 64, "XNodeRec must be 64 B");
 
 // The node triangle-box skip (internal nodes too, DevScene::xnodes):
 // 1 = the finite-slab walks read xnodes, 0 = mnodes (leaves only).
+// config 5 without per-ray ids: one pixel's rays walked as a pool of
+// subtree pieces (occl_coop, vrt_kernels.hip) instead of ray compaction
+// (SpillQueues, resume rounds); 0 restores the compaction
+#ifndef VRT_SEC_COOP
+#define VRT_SEC_COOP 1
+#endif
 #ifndef VRT_NODE_BOX
 #define VRT_NODE_BOX 1
 #endif

@@ -1388,6 +1388,190 @@ __device__ __forceinline__ int occl_dispatch_spill(const DevScene &sc, const Ray
         return occl_walk<false, kS, kR64, false, true>(sc, r, stk, w, spill_t);
 }
 
+// ---------------------------------------------------------------------------
+// Cooperative occlusion walk of one pixel's rays (config 5, VRT_SEC_COOP).
+// Only each ray's boolean is needed, and a ray's walk state is a set of
+// independent subtrees -- the children left in the block it is walking and
+// every DFS stack entry (a block and its children still to visit) -- whose
+// answer is the OR of theirs (ray_march returns true iff some leaf below a
+// box-passing path holds a triangle that passes, whatever the order,
+// occl_walk).  So the wave's lanes are a pool: lane l starts on ray l (slot
+// l; lanes >= nrays start idle), and whenever some lanes are idle, each busy
+// lane that has work to spare hands one piece to one idle lane -- its
+// bottom stack entry (the shallowest pending block, the largest subtree
+// set), or else the upper half of the children left in its current block --
+// through an LDS mailbox, with the ray's slot; the receiver loads that ray's
+// direction from LDS and walks the piece with an empty stack of its own.  A
+// leaf that passes marks its ray's slot hit (an LDS flag, then a ballot);
+// every lane walking a piece of a hit ray drops it.  The pixel is done when
+// no lane has work.  Returns the hit rays' mask (bit = slot).  The slab, box
+// and MT tests are occl_walk's, so every ray's boolean is unchanged; only
+// the work after a ray's first passing leaf differs (pieces of it walked in
+// parallel until the flag is seen at their next leaf).
+// dirs: the pixel's ray directions (LDS, [64][3]); mbox: 64 uint2 (LDS);
+// hflag: 64 words (LDS); stk: this lane's LDS stack column (stride kS).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_id()
+{
+        int lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        return (uint32_t)lane;
+}
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool kFast, int kS, bool kR64, bool kFin>
+__device__ __forceinline__ uint64_t occl_coop(const DevScene &sc, f3 o, float tmin, const float (*dirs)[3],
+                                              uint2 *mbox, uint32_t *hflag, uint2 *stk, int nrays)
+{
+        constexpr bool kLB = kFast && kFin;
+        constexpr bool kNB = kLB && VRT_NODE_BOX;
+        const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
+        const uint32_t lane = lane_id();
+        uint32_t slot = lane;
+        RayK r = make_rayk(o, mk3(dirs[slot][0], dirs[slot][1], dirs[slot][2]), tmin, kFltMax);
+        const bool lbok = kLB && __all(leaf_box_ok(sc, r));  // one origin: uniform
+        uint32_t s = dir_signs(r);
+        uint32_t base = 0, mask = 0;
+        int sp = 0, bot = 0;
+        bool busy = false, hit = false;
+        if ((int)lane < nrays) {
+                OcclState w;
+                const int st = occl_start<kFast, kR64, kFin>(sc, r, w);
+                hit = st == kOcclHit;
+                busy = st == kOcclWalk;
+                base = w.base;
+                mask = w.mask;
+        }
+        hflag[lane] = hit ? 1u : 0u;
+        uint64_t hitm = __ballot(hit);
+        for (;;) {
+                // hand work to idle lanes (wave-uniform decisions)
+                const uint64_t idle = __ballot(!busy);
+                if (idle == ~0ull)
+                        break;
+                const bool spare = busy && (sp > bot || __popc(mask) >= 2);
+                const uint64_t don = __ballot(spare);
+                if (idle != 0ull && don != 0ull) {
+                        const uint32_t n = min((uint32_t)__popcll(idle), (uint32_t)__popcll(don));
+                        if (spare) {
+                                const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(don >> 32),
+                                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)don, 0u));
+                                if (k < n) {
+                                        uint2 e;
+                                        if (sp > bot) {
+                                                e = stk[bot * kS];
+                                                ++bot;
+                                        } else {
+                                                // keep the lower half of the children left, give the rest
+                                                uint32_t give = mask;
+                                                for (int c = (__popc(mask) + 1) >> 1; c > 0; --c)
+                                                        give &= give - 1u;
+                                                mask ^= give;
+                                                e = make_uint2(base, give);
+                                        }
+                                        mbox[k] = make_uint2(e.x, e.y | (slot << 8));
+                                }
+                        }
+                        wave_lds_sync();
+                        if (!busy) {
+                                const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                                if (k < n) {
+                                        const uint2 e = mbox[k];
+                                        slot = e.y >> 8;
+                                        base = e.x;
+                                        mask = e.y & 0xFFu;
+                                        sp = bot = 0;
+                                        busy = true;
+                                        r = make_rayk(o, mk3(dirs[slot][0], dirs[slot][1], dirs[slot][2]), tmin,
+                                                      kFltMax);
+                                        s = dir_signs(r);
+                                }
+                        }
+                        wave_lds_sync();  // the mailbox is rewritten next time
+                }
+                // advance to the next non-empty leaf of this lane's piece (as occl_walk)
+                bool leaf = false;
+                uint32_t nref = 0, b = 0;
+                if (busy) {
+                        float bmin[3], bmax[3];
+                        uint32_t a;
+                        for (;;) {
+                                if (mask == 0) {
+                                        if (sp == bot)
+                                                break;
+                                        --sp;
+                                        const uint2 e = stk[sp * kS];
+                                        base = e.x;
+                                        mask = e.y;
+                                        if (!VRT_POP_VISIT)
+                                                continue;
+                                }
+                                const uint32_t ci = (uint32_t)__builtin_ctz(mask) ^ s;
+                                mask &= mask - 1u;
+                                if (kNB) {
+                                        float tmn[3], tmx[3];
+                                        load_xnode(sc.xnodes, base + ci, bmin, bmax, a, b, tmn, tmx);
+                                        if (lbok && !line_meets_box(tmn, tmx, r))
+                                                continue;
+                                } else {
+                                        load_node(nodes, base + ci, bmin, bmax, a, b);
+                                }
+                                if (!(a & kLeafBit)) {
+                                        if (mask) {
+                                                stk[sp * kS] = make_uint2(base, mask);
+                                                ++sp;
+                                        }
+                                        mask = xor_permute8(child_hit_mask<kFast, kFin>(bmin, bmax, r) & b, s);
+                                        base = a;
+                                        continue;
+                                }
+                                nref = a & ~kLeafBit;
+                                if (kLB && !kNB && lbok && !line_meets_box(bmin, bmax, r))
+                                        continue;
+                                leaf = true;
+                                break;
+                        }
+                        if (!leaf) {
+                                busy = false;
+                                sp = bot = 0;
+                        }
+                }
+                hit = false;
+                if (leaf) {
+                        bool done = false;
+                        if (kR64 && VRT_SEC_UNI) {
+                                const uint32_t f0 = __builtin_amdgcn_readfirstlane(b);
+                                const uint32_t n0 = __builtin_amdgcn_readfirstlane(nref);
+                                if (__all(b == f0 && nref == n0)) {
+                                        hit = leaf_any<true>(static_cast<const RefRec64 *>(sc.refs) + f0, 0, n0, r);
+                                        done = true;
+                                }
+                        }
+                        if (!done)
+                                hit = leaf_any<kR64>(sc.refs, b, nref, r);
+                }
+                if (__ballot(hit) != 0ull) {
+                        if (hit)
+                                hflag[slot] = 1u;
+                        wave_lds_sync();
+                        hitm = __ballot(hflag[lane] != 0u);
+                        if (busy && ((hitm >> slot) & 1ull)) {  // this ray is decided
+                                busy = false;
+                                mask = 0;
+                                sp = bot = 0;
+                        }
+                }
+        }
+        return hitm;
+}
+
 // One stopped ray's record (SpillRec): its pixel, sample, direction and walk
 // state, the stack entries copied out of the lane's LDS column.
 template <int kS>
@@ -1574,11 +1758,22 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         ty += p.ty0;
         // pixel, sample and Camera::gen_rays4 direction (VRT/camera.cc:95-112)
         // of lane l
+#ifndef VRT_UNIT_ROWS
+#define VRT_UNIT_ROWS 0
+#endif
         auto sample_of = [&](int l, int &px, int &py, int &s, int &lx, int &ly) {
                 s = l & 3;
                 const int pix = l >> 2;
-                lx = (wave & 1) * 4 + (pix & 3);
-                ly = (wave >> 1) * 4 + (pix >> 2);
+                if (VRT_UNIT_ROWS) {
+                        // unit = 2 whole tile rows (8x2 pixels): each row's 8
+                        // pixels are 96 B = three whole 32-B sectors of the film
+                        lx = pix & 7;
+                        ly = wave * 2 + (pix >> 3);
+                } else {
+                        // unit = a 4x4 quadrant of the tile
+                        lx = (wave & 1) * 4 + (pix & 3);
+                        ly = (wave >> 1) * 4 + (pix >> 2);
+                }
                 px = tx * 8 + lx;
                 py = ty * 8 + ly;
                 // opaque per unit, as the deal's sizes above: the film size and
@@ -2014,7 +2209,7 @@ constexpr int kSecPBlock = 256;
 // ray's hit boolean -> the occlusion walk (ray_occluded), same booleans.
 template <bool kR64, bool kAny, int kS>
 __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_t k, int lane, uint2 *stk,
-                                                float (*pts)[3], SpillCursor &cur)
+                                                float (*pts)[3], uint2 *mbox, uint32_t *hflag, SpillCursor &cur)
 {
         // lane id re-read per pixel (not held across k_secondary_p's loop)
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
@@ -2066,6 +2261,30 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (kAny && VRT_SEC_COOP) {
+                // the pixel's rays as one pool of subtree walks (occl_coop):
+                // directions into LDS (over the sphere points), then the
+                // fast / exact walk chosen for the whole pixel
+                bool ok = true;
+                if (lane < p.spp) {
+                        const f3 d = normalize(nrm + mk3(pts[lane][0], pts[lane][1], pts[lane][2]));
+                        pts[lane][0] = d.x;
+                        pts[lane][1] = d.y;
+                        pts[lane][2] = d.z;
+                        const RayK r = make_rayk(hp, d, p.res, kFltMax);
+                        ok = p.sc.fast_ok && fast_ok(r) && (!VRT_FIN || fin_ok(r));
+                }
+                wave_lds_sync();
+                const uint64_t hm =
+                        __all(ok) ? occl_coop<true, kS, kR64, VRT_FIN != 0>(p.sc, hp, p.res, pts, mbox, hflag, stk, p.spp)
+                                  : occl_coop<false, kS, kR64, false>(p.sc, hp, p.res, pts, mbox, hflag, stk, p.spp);
+                if (p.s_hit && lane < p.spp)
+                        p.s_hit[vi * (size_t)p.spp + lane] = (int32_t)((hm >> lane) & 1ull);
+                if (lane == 0)
+                        p.vis[vi] = (float)(p.spp - (int)__popcll(hm)) / (float)p.spp;
+                wave_lds_sync();  // pts / mbox / hflag are rewritten by the next pixel
+                return;
+        }
         // with compaction: the rays still walking when fewer than t_first
         // lanes are go to queue 0 (SpillQueues)
         const uint32_t t = kAny ? spill_reserve(p.sq, p.sq.ctr, p.sq.fill[0], cur, p.sq.t_first) : 0u;
@@ -2197,12 +2416,16 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
 {
         __shared__ uint2 stk[kStack * kSecBlock];
         __shared__ float pts[VRT_SEC_WAVES][64][3];
+        __shared__ uint2 mbox[kAny && VRT_SEC_COOP ? VRT_SEC_WAVES : 1][64];
+        __shared__ uint32_t hflag[kAny && VRT_SEC_COOP ? VRT_SEC_WAVES : 1][64];
         const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
         const int64_t k = (int64_t)blockIdx.x * VRT_SEC_WAVES + wave;
         SpillCursor cur;  // no compaction in the one-pixel-per-wave grid (p.sq.nchunks == 0)
         cur.chunk = kSpillNone;
         cur.fill = 0;
-        secondary_pixel<kR64, kAny, kSecBlock>(p, k, lane, stk + tid, pts[wave], cur);
+        constexpr int mw = kAny && VRT_SEC_COOP ? 1 : 0;
+        secondary_pixel<kR64, kAny, kSecBlock>(p, k, lane, stk + tid, pts[wave], mbox[wave * mw], hflag[wave * mw],
+                                               cur);
 }
 
 // Persistent config 5: one resident generation of 4-wave workgroups; each
@@ -2215,6 +2438,9 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
 {
         __shared__ uint2 stk[kStack * kSecPBlock];
         __shared__ float pts[kSecPBlock / 64][64][3];
+        __shared__ uint2 mbox[kAny && VRT_SEC_COOP ? kSecPBlock / 64 : 1][64];
+        __shared__ uint32_t hflag[kAny && VRT_SEC_COOP ? kSecPBlock / 64 : 1][64];
+        constexpr int mw = kAny && VRT_SEC_COOP ? 1 : 0;
         const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
         const int xcd = blockIdx.x & 7;
         SpillCursor cur;
@@ -2231,10 +2457,10 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
                                 break;
                         secondary_pixel<kR64, kAny, kSecPBlock>(
                                 p, (int64_t)slice_unit(p.units, x, (int)u, VRT_SEC_SLICE_CHUNK), lane, stk + tid,
-                                pts[wave], cur);
+                                pts[wave], mbox[wave * mw], hflag[wave * mw], cur);
                 }
         }
-        if (kAny)
+        if (kAny && !VRT_SEC_COOP)
                 spill_close(p.sq.fill[0], p.sq.ctr, cur);
 }
 
@@ -2307,7 +2533,7 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                 const int g = (int)std::min<int64_t>(cap, ((waves + 3) / 4 + 7) & ~7LL);
                 void (*kern)(SecondaryParams) = w ? (any ? k_secondary_p<true, true> : k_secondary_p<true, false>)
                                                   : (any ? k_secondary_p<false, true> : k_secondary_p<false, false>);
-                const bool spill = any && sq && sq->t_first > 0 && sq->nchunks > 0;
+                const bool spill = !VRT_SEC_COOP && any && sq && sq->t_first > 0 && sq->nchunks > 0;
                 if (spill) {
                         sp.sq = *sq;
                         if (rp.test_flags & VRT_TEST_SPILL_ALL)  // test hook: stop at the first ray's end
