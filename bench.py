@@ -102,7 +102,11 @@ def pmc_per_kernel(out_dir, steps):
                 kn = short_name(r["Kernel_Name"])
                 by_k.setdefault(kn, []).append(r)
                 meta[kn] = {"kernel": r["Kernel_Name"], "grid": int(r["Grid_Size"]), "wg": int(r["Workgroup_Size"]),
-                            "lds": int(r["LDS_Block_Size"]), "vgpr": int(r["VGPR_Count"]),
+                            "lds": int(r["LDS_Block_Size"]),
+                            # rocprofv3's VGPR_Count on gfx950 is half the allocated
+                            # VGPRs (40 / 48 / 32 for the 80 / 96 / 64 the ISA
+                            # reports for k_render_p / k_light / k_cones_film): both
+                            "vgpr": 2 * int(r["VGPR_Count"]), "rocprof_vgpr_count": int(r["VGPR_Count"]),
                             "sgpr": int(r["SGPR_Count"]), "scratch": int(r["Scratch_Size"])}
             for kn, rows in by_k.items():
                 ids = sorted({int(r["Dispatch_Id"]) for r in rows})

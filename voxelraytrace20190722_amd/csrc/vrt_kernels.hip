@@ -123,14 +123,28 @@ __device__ __forceinline__ void load_node_st(const NodeRec *__restrict__ nodes, 
 #ifndef VRT_PHASE_STAMPS
 #define VRT_PHASE_STAMPS 0
 #endif
-#if VRT_PHASE_STAMPS
-__device__ unsigned long long g_phase[16];
+// wave reductions (every lane of the wave active)
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 {
         for (int o = 32; o > 0; o >>= 1)
                 v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
         return v;
 }
+__device__ __forceinline__ uint32_t lane_id()
+{
+        int lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        return (uint32_t)lane;
+}
+// LDS written by some lanes of a wave, then read by others of the same wave
+__device__ __forceinline__ void wave_lds_sync()
+{
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+#if VRT_PHASE_STAMPS
+__device__ unsigned long long g_phase[16];
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
 {
         for (int o = 32; o > 0; o >>= 1)
@@ -543,7 +557,7 @@ __device__ __forceinline__ bool first_min_takes(bool any, float best, float dept
 // (q0..q2 = the 48-B RefRec48, or q0 + qd1..qd3 = the RefRec64) and the
 // first-minimum update of the best hit (any, best, best_t, m.tri/u/v).
 template <bool kR64>
-__device__ __forceinline__ void mt_record(const float4 q0, const float4 q1, const float4 q2, const double2 qd1,
+__device__ __forceinline__ bool mt_record(const float4 q0, const float4 q1, const float4 q2, const double2 qd1,
                                           const double2 qd2, const double2 qd3, const RayK &r, bool &any,
                                           float &best, float &best_t, MarchResult &m)
 {
@@ -568,7 +582,7 @@ __device__ __forceinline__ void mt_record(const float4 q0, const float4 q1, cons
         // det
         const double det = e1x * px + e1y * py + e1z * pz;
         if (!(det > 0.000001) && !(det < -0.000001))
-                return;  // parallel
+                return false;  // parallel
 #ifndef VRT_MT_RECVT
 #define VRT_MT_RECVT 1
 #endif
@@ -592,23 +606,23 @@ __device__ __forceinline__ void mt_record(const float4 q0, const float4 q1, cons
         // the same accept/reject decisions, without divergent sign branches
         const double sdet = pos ? det : -det, suu = pos ? uu : -uu;
         if (suu < 0.0 || suu > sdet)
-                return;
+                return false;
         const double qx = ty * e1z - tz * e1y;
         const double qy = tz * e1x - tx * e1z;
         const double qz = tx * e1y - ty * e1x;
         const double vv = dx * qx + dy * qy + dz * qz;
         const double svv = pos ? vv : -vv;
         if (svv < 0.0 || suu + svv > sdet)
-                return;
+                return false;
 #else
         if (pos ? (uu < 0.0 || uu > det) : (uu > 0.0 || uu < det))
-                return;
+                return false;
         const double qx = ty * e1z - tz * e1y;
         const double qy = tz * e1x - tx * e1z;
         const double qz = tx * e1y - ty * e1x;
         const double vv = dx * qx + dy * qy + dz * qz;
         if (pos ? (vv < 0.0 || uu + vv > det) : (vv > 0.0 || uu + vv < det))
-                return;
+                return false;
 #endif
         const double inv_det = 1.0 / det;
         const double t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
@@ -625,7 +639,9 @@ __device__ __forceinline__ void mt_record(const float4 q0, const float4 q1, cons
                 m.tri = __float_as_uint(kR64 ? q0.w : q2.y);
                 m.u = fu;
                 m.v = fv;
+                return true;
         }
+        return false;
 }
 
 // ray_march_isect (VRT/voxel_octree.cc:99-129) over one leaf's records, with
@@ -760,12 +776,100 @@ __device__ __forceinline__ bool leaf_box_ok(const DevScene &sc, const RayK &r)
                fabsf(r.o.z - sc.lb_center[2]) <= sc.lb_reach;
 }
 
+// ---------------------------------------------------------------------------
+// Cooperative leaf phase (kCL, the light pass and the trace render's primary
+// march over large-leaf scenes): when only a few lanes of a full wave hold a
+// leaf (the tail of long walks -- near-vertical light rays test up to ~2,500
+// triangles over a few dozen leaves), the whole wave tests each such leaf's
+// records for that lane's ray, 64 records at a time, and reduces them to
+// ray_march_isect's answer: the first strict minimum of depth in record order
+// (VRT/voxel_octree.cc:122-125) = the smallest (depth, record index), depth
+// >= +0 ordered by its bits.  A NaN depth as some lane's first hit (the only
+// way a NaN can be the serial answer) sends that leaf to the serial loop.
+// The winning record is re-run by the owning lane (any = false), so tri, u, v
+// and t are the serial loop's values.  Returns the owning lane's leaf result.
+// ---------------------------------------------------------------------------
+#ifndef VRT_CL
+#define VRT_CL 1         // the light pass / trace primary marches use it
+#endif
+#ifndef VRT_CL_LANES
+#define VRT_CL_LANES 8   // leaf lanes at most for the cooperative phase
+#endif
+#ifndef VRT_CL_RATIO
+#define VRT_CL_RATIO 4   // ... and the longest leaf >= this x their number (records)
+#endif
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
+{
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+                const uint64_t w = (uint64_t)__shfl_xor((long long)v, o, 64);
+                v = w < v ? w : v;
+        }
+        return v;
+}
+
+template <bool kR64>
+__device__ __forceinline__ bool coop_leaves(const DevScene &sc, const RayK &r, uint64_t lm, uint32_t first,
+                                            uint32_t nref, MarchResult &m)
+{
+        const uint32_t lane = lane_id();
+        bool mine = false;
+        while (lm) {  // wave-uniform
+                const int L = __builtin_ctzll(lm);
+                lm &= lm - 1ull;
+                const uint32_t f = __builtin_amdgcn_readlane(first, L);
+                const uint32_t n = __builtin_amdgcn_readlane(nref, L);
+                RayK rl;
+                rl.o.x = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.o.x), L));
+                rl.o.y = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.o.y), L));
+                rl.o.z = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.o.z), L));
+                rl.d.x = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.d.x), L));
+                rl.d.y = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.d.y), L));
+                rl.d.z = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.d.z), L));
+                bool any = false;
+                float best = 0.f, bt = 0.f;
+                uint32_t kb = 0;
+                MarchResult mm;
+                for (uint32_t k = lane; k < n; k += 64) {
+                        const float4 *q = kR64 ? reinterpret_cast<const float4 *>(static_cast<const RefRec64 *>(sc.refs) + f + k)
+                                               : reinterpret_cast<const float4 *>(static_cast<const RefRec48 *>(sc.refs) + f + k);
+                        const double2 *qd = reinterpret_cast<const double2 *>(q);
+                        const float4 q0 = q[0];
+                        float4 q1 = q0, q2 = q0;
+                        double2 qd1 = {}, qd2 = {}, qd3 = {};
+                        if (kR64) {
+                                qd1 = qd[1];
+                                qd2 = qd[2];
+                                qd3 = qd[3];
+                        } else {
+                                q1 = q[1];
+                                q2 = q[2];
+                        }
+                        if (mt_record<kR64>(q0, q1, q2, qd1, qd2, qd3, rl, any, best, bt, mm))
+                                kb = k;
+                }
+                if (__ballot(any && isnan(best)) != 0ull) {
+                        if ((int)lane == L)  // the serial loop decides this leaf
+                                mine = leaf_isect_v2<false, kR64>(sc.refs, first, nref, r, m);
+                        continue;
+                }
+                const uint64_t key = any ? ((uint64_t)__float_as_uint(best) << 32) | kb : ~0ull;
+                const uint64_t kmin = wave_min_u64(key);
+                if (kmin != ~0ull && (int)lane == L) {
+                        // the winner again, as the serial loop's taking step
+                        mine = leaf_isect_v2<false, kR64>(sc.refs, first + (uint32_t)kmin, 1u, r, m);
+                }
+        }
+        return mine;
+}
+
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).  The finite-slab fast walk (kStd == 2)
 // reads DevScene::mnodes and skips a leaf whose triangles' box the ray's
 // line misses (no triangle of it can pass; the leaf is left as the reference
 // leaves it, with no record).
-template <bool kCount, bool kFast, int kS, int kStd, bool kUni, bool kR64, int kNS = 0>
+template <bool kCount, bool kFast, int kS, int kStd, bool kUni, bool kR64, int kNS = 0, bool kCL = false>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint2 *stk,
                                           uint32_t *stk_aux,
@@ -812,6 +916,11 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         uint32_t d_it = 0, d_lp = 0, d_tri = 0, d_lpmax = 0, d_lpsum = 0, d_phmax = 0;
         unsigned long long d_tin = 0, d_tleaf = 0;
 #endif
+        // kCL: lanes stay in the loop when their walk ends (done), so that
+        // the whole wave can take part in a cooperative leaf phase
+        const bool cl_full = kCL && __ballot(1) == ~0ull;
+        bool done = false;
+        uint32_t sib_pf = 0;  // VRT_SIB_PF: the prefetches' words, kept live
         for (;;) {
                 bool leaf = false;
                 uint32_t node = 0, nref = 0;
@@ -822,6 +931,8 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
 #define VRT_POP_VISIT 1
 #endif
                 for (;;) {
+                        if (kCL && done)
+                                break;
 #if VRT_PHASE_STAMPS
                         ++d_it;
 #endif
@@ -853,6 +964,11 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                 path_rem[depth * kS] = 7u - ((fpos >> (3 * ci)) & 7u);
                         if (kNB) {
                                 float tmn[3], tmx[3];
+#ifndef VRT_SIB_PF
+#define VRT_SIB_PF 0
+#endif
+                                if (VRT_SIB_PF && cnt > 0)  // the next sibling's record towards the caches
+                                        sib_pf ^= reinterpret_cast<const uint32_t *>(sc.xnodes + base + (order & 7u))[0];
                                 load_xnode(sc.xnodes, node, bmin, bmax, a, b, tmn, tmx);
                                 if (lbok && !line_meets_box(tmn, tmx, r))
                                         continue;  // no triangle below this node can pass
@@ -899,6 +1015,27 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         d_phmax += d_lpmax;
                 }
 #endif
+                if (kCL) {
+                        done = done || !leaf;
+                        if (__ballot(!done) == 0ull)
+                                break;
+                        const uint64_t lm = __ballot(leaf);
+                        const uint32_t nl = (uint32_t)__popcll(lm);
+                        bool coop = cl_full && nl <= VRT_CL_LANES;
+                        if (coop)
+                                coop = wave_max_u32(leaf ? nref : 0u) >= (uint32_t)VRT_CL_RATIO * nl;
+                        bool lh = false;
+                        if (coop)
+                                lh = coop_leaves<kR64>(sc, r, lm, b, nref, m);
+                        else if (leaf)
+                                lh = leaf_isect<kCount, kUni, kR64>(sc, b, nref, r, m);
+                        if (leaf && lh) {
+                                m.hit = true;
+                                m.node = node;
+                                done = true;
+                        }
+                        continue;
+                }
                 if (!leaf)
                         break;
 #if VRT_PHASE_STAMPS
@@ -995,6 +1132,8 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 }
         }
 #endif
+        if (VRT_SIB_PF)
+                asm volatile("" : : "v"(sib_pf));
         if (kCount) {
                 // 1 root test + 8 per expanded node, minus the children the
                 // reference never popped on the path it stopped on.
@@ -1044,7 +1183,7 @@ __device__ __forceinline__ bool fin_ok(const RayK &r)
                fabsf(r.dinv.z) <= 0x1p64f;
 }
 
-template <bool kCount, int kS, bool kUni, bool kR64, int kNS = 0>
+template <bool kCount, int kS, bool kUni, bool kR64, int kNS = 0, bool kCL = false>
 __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const RayK &r,
                                                    uint2 *sb, uint32_t *sa, uint32_t *pr,
                                                    MarchResult &m)
@@ -1054,7 +1193,7 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
 #endif
         if (__all(sc.fast_ok && fast_ok(r))) {
                 if (VRT_FIN && !kCount && __all(fin_ok(r)))
-                        ray_march<kCount, true, kS, 2, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, 2, kUni, kR64, kNS, kCL>(sc, r, sb, sa, pr, m);
                 else if (!VRT_FIN && VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
                         ray_march<kCount, true, kS, 1, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
                 else
@@ -1411,20 +1550,6 @@ __device__ __forceinline__ int occl_dispatch_spill(const DevScene &sc, const Ray
 // dirs: the pixel's ray directions (LDS, [64][3]); mbox: 64 uint2 (LDS);
 // hflag: 64 words (LDS); stk: this lane's LDS stack column (stride kS).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lane_id()
-{
-        int lane;
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-        return (uint32_t)lane;
-}
-
-__device__ __forceinline__ void wave_lds_sync()
-{
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 template <bool kFast, int kS, bool kR64, bool kFin>
 __device__ __forceinline__ uint64_t occl_coop(const DevScene &sc, f3 o, float tmin, const float (*dirs)[3],
                                               uint2 *mbox, uint32_t *hflag, uint2 *stk, int nrays)
@@ -3091,7 +3216,7 @@ __device__ __forceinline__ void light_unit(const LightParams &p, uint2 *stk, int
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock, true, kR64, 0, VRT_CL>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         if (!m.hit)
                 return;
         // canonical order: render_mt task t = tx*8 + ty (VRT/camera.h:50-56)
@@ -3588,6 +3713,37 @@ __device__ __forceinline__ f3 cone_trace_isect(const TraceParams &p, f3 hit, f3 
         return diffuse;
 }
 
+// cone_trace_isect over a sample record (hit point in rec[0].xyz, normal in
+// rec[1].xyz): the same operations in the same order, the record re-read per
+// cone (volatile asm keeps the compiler from hoisting it across the marches)
+__device__ __forceinline__ f3 cone_trace_rec(const TraceParams &p, const float4 *rec)
+{
+        const float hx[6] = { 0.000000f, 0.000000f, 0.823639f, 0.509037f, -0.509037f, -0.823639f };
+        const float hy[6] = { 0.000000f, 0.866025f, 0.267617f, -0.700629f, -0.700629f, 0.267617f };
+        const float hz[6] = { 1.0f, 0.5f, 0.5f, 0.5f, 0.5f, 0.5f };
+        const float hw[6] = { 0.25f, 0.15f, 0.15f, 0.15f, 0.15f, 0.15f };
+        f3 diffuse = mk3(0.f, 0.f, 0.f);
+        for (int i = 0; i < 6; ++i) {
+                const float4 *q = rec;
+                asm volatile("" : "+v"(q));
+                const float4 r0 = q[0], r1 = q[1];
+                const f3 hit = mk3(r0.x, r0.y, r0.z), n = mk3(r1.x, r1.y, r1.z);
+                const float sg = (0.0f > n.z) ? -1.0f : 1.0f;
+                const float a0 = -1.0f / (sg + n.z);
+                const float a1 = n.x * n.y * a0;
+                const f3 t = mk3(1.0f + sg * n.x * n.x * a0, sg * a1, -sg * n.x);
+                const f3 bb = mk3(a1, sg + n.y * n.y * a0, -n.y);
+                f3 r = mk3(0.f, 0.f, 0.f);
+                r = r + t * hx[i];
+                r = r + bb * hy[i];
+                r = r + n * hz[i];
+                const f3 cd = normalize(r);
+                const f3 cm = cone_march(p, hit, cd);
+                diffuse = diffuse + cm * hw[i];
+        }
+        return diffuse;
+}
+
 // trace(root, ray, 5, true) per sample + Film::add(c * .25f)
 // (VRT/main.cc:10-30, 118-123)
 template <bool kR64>
@@ -3605,7 +3761,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock, true, kR64, 0, VRT_CL>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         f3 col;
         if (m.hit) {
                 f3 nrm;
@@ -3663,7 +3819,7 @@ __device__ __forceinline__ void trace_prim_unit(const TraceParams &p, uint2 *stk
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock, true, kR64, 0, VRT_CL>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         float4 *o = p.rec + 4 * slot;
         if (m.hit) {
                 f3 nrm;
@@ -3698,7 +3854,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
 // pixel is written once: each sample record is read once, and no per-cone
 // result goes through memory.
 #ifndef VRT_CONES_WAVES_PER_EU
-#define VRT_CONES_WAVES_PER_EU 8  // 64 VGPRs; the spills are per cone, outside the step loop
+#define VRT_CONES_WAVES_PER_EU 7  // 70 VGPRs, no scratch (with VRT_CONES_RELOAD; 8 waves: 24 B/lane)
 #endif
 __global__ __launch_bounds__(64, VRT_CONES_WAVES_PER_EU) void k_cones_film(TraceParams p)
 {
@@ -3706,27 +3862,41 @@ __global__ __launch_bounds__(64, VRT_CONES_WAVES_PER_EU) void k_cones_film(Trace
         constexpr int kQ = 4 / VRT_RENDER_WAVES;
         if (u >= p.r.tiles_this_rank * kQ)
                 return;
+        const int64_t slot = (int64_t)u * 64 + threadIdx.x;
+#ifndef VRT_CONES_RELOAD
+#define VRT_CONES_RELOAD 1
+#endif
+        f3 col;
+        if (p.rec[4 * slot + 0].w != 0.f) {
+                f3 diffuse;
+                if (VRT_CONES_RELOAD) {
+                        // cone_trace_isect with the hit point and normal read
+                        // from the sample record per cone (L2 hits) and the
+                        // basis remade per cone -- the same values -- rather
+                        // than held in registers across the 6 cone marches
+                        diffuse = cone_trace_rec(p, p.rec + 4 * slot);
+                } else {
+                        const float4 r0 = p.rec[4 * slot + 0], r1 = p.rec[4 * slot + 1];
+                        diffuse = cone_trace_isect(p, mk3(r0.x, r0.y, r0.z), mk3(r1.x, r1.y, r1.z));
+                }
+                const float4 r2 = p.rec[4 * slot + 2], r3 = p.rec[4 * slot + 3];
+                const f3 lsum = diffuse + mk3(r3.x, r3.y, r3.z);
+                col = mk3(r2.x * lsum.x, r2.y * lsum.y, r2.z * lsum.z);
+        } else {
+                const float4 r2 = p.rec[4 * slot + 2];
+                col = mk3(r2.x, r2.y, r2.z);
+        }
+        // the pixel of this lane, made after the cone marches (not held across them)
         const int lane = threadIdx.x;
-        const int64_t slot = (int64_t)u * 64 + lane;
         const int k = u / kQ, wave = u % kQ;
         int tx, ty;
         deal_tile(tile_deal(p.r.ntx, p.r.nty, p.r.nranks), p.r.rank, k, tx, ty);
         const int s = lane & 3, pix = lane >> 2;
         const int lx = (wave & 1) * 4 + (pix & 3), ly = (wave >> 1) * 4 + (pix >> 2);
         const int px = tx * 8 + lx, py = ty * 8 + ly;
-        const float4 r0 = p.rec[4 * slot + 0], r2 = p.rec[4 * slot + 2];
-        f3 col;
-        if (r0.w != 0.f) {
-                const float4 r1 = p.rec[4 * slot + 1], r3 = p.rec[4 * slot + 3];
-                const f3 diffuse = cone_trace_isect(p, mk3(r0.x, r0.y, r0.z), mk3(r1.x, r1.y, r1.z));
-                const f3 lsum = diffuse + mk3(r3.x, r3.y, r3.z);
-                col = mk3(r2.x * lsum.x, r2.y * lsum.y, r2.z * lsum.z);
-        } else {
-                col = mk3(r2.x, r2.y, r2.z);
-        }
         const size_t si = ((size_t)py * p.r.cam.nx + px) * 4 + s;
         if (p.r.so.hit)
-                p.r.so.hit[si] = r0.w != 0.f ? 1 : 0;
+                p.r.so.hit[si] = p.rec[4 * slot + 0].w != 0.f ? 1 : 0;
         if (p.r.so.rgb) {
                 p.r.so.rgb[3 * si + 0] = col.x;
                 p.r.so.rgb[3 * si + 1] = col.y;
