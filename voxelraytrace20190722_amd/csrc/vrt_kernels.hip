@@ -1340,16 +1340,34 @@ __device__ __forceinline__ uint32_t xor_permute8(uint32_t m, uint32_t s)
 
 // true iff some record of the leaf passes intersect_triangle3's tests
 // (VRT/raytri.cc:197-249, the same operations as leaf_isect_v2)
-template <bool kR64>
-__device__ __forceinline__ bool leaf_any(const void *__restrict__ refs, uint32_t first, uint32_t n, const RayK &r)
+// (the records' float4 / double2 views in the base pointer's address space)
+template <typename B>
+struct RecView {
+        typedef const float4 F4;
+        typedef const double2 D2;
+};
+#if defined(__HIP_DEVICE_COMPILE__)
+template <>
+struct RecView<const VRT_AS1 char> {
+        typedef const VRT_AS1 float4 F4;
+        typedef const VRT_AS1 double2 D2;
+};
+#endif
+
+template <bool kR64, typename B = const char>
+__device__ __forceinline__ bool leaf_any(const void *__restrict__ refs, uint32_t first, uint32_t n, const RayK &r,
+                                         B *base = nullptr)
 {
+        typedef typename RecView<B>::F4 F4;
+        typedef typename RecView<B>::D2 D2;
+        if (!base)
+                base = (B *)refs;
         const double dx = r.d.x, dy = r.d.y, dz = r.d.z;
         for (uint32_t k = 0; k < n; ++k) {
-                const float4 *q = kR64 ? reinterpret_cast<const float4 *>(static_cast<const RefRec64 *>(refs) + first + k)
-                                       : reinterpret_cast<const float4 *>(static_cast<const RefRec48 *>(refs) + first + k);
+                F4 *q = reinterpret_cast<F4 *>(base + (size_t)(first + k) * (kR64 ? sizeof(RefRec64) : sizeof(RefRec48)));
                 const float4 q0 = q[0];
                 const double v0x = q0.x, v0y = q0.y, v0z = q0.z;
-                const double2 *qd = reinterpret_cast<const double2 *>(q);
+                D2 *qd = reinterpret_cast<D2 *>(q);
                 float4 q1, q2;
                 double2 qd1, qd2, qd3;
                 double e2x, e2y, e2z;
@@ -1592,6 +1610,14 @@ __device__ __forceinline__ uint64_t occl_coop(const DevScene &sc, f3 o, float tm
         constexpr bool kLB = kFast && kFin;
         constexpr bool kNB = kLB && VRT_NODE_BOX;
         const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
+        // the record bases held as values (VRT_PIN_SEC, as VRT_PIN_XN in ray_march)
+#ifndef VRT_PIN_SEC
+#define VRT_PIN_SEC 0
+#endif
+        xnode_gptr xn = (xnode_gptr)sc.xnodes;
+        const VRT_AS1 char *rb = (const VRT_AS1 char *)sc.refs;
+        if (VRT_PIN_SEC)
+                asm volatile("" : "+s"(xn), "+s"(rb));
         const uint32_t lane = lane_id();
         uint32_t slot = lane;
         RayK r = make_rayk(o, mk3(dirs[slot][0], dirs[slot][1], dirs[slot][2]), tmin, kFltMax);
@@ -1677,7 +1703,7 @@ __device__ __forceinline__ uint64_t occl_coop(const DevScene &sc, f3 o, float tm
                                 mask &= mask - 1u;
                                 if (kNB) {
                                         float tmn[3], tmx[3];
-                                        load_xnode(sc.xnodes, base + ci, bmin, bmax, a, b, tmn, tmx);
+                                        load_xnode(xn, base + ci, bmin, bmax, a, b, tmn, tmx);
                                         if (lbok && !line_meets_box(tmn, tmx, r))
                                                 continue;
                                 } else {
@@ -1710,12 +1736,12 @@ __device__ __forceinline__ uint64_t occl_coop(const DevScene &sc, f3 o, float tm
                                 const uint32_t f0 = __builtin_amdgcn_readfirstlane(b);
                                 const uint32_t n0 = __builtin_amdgcn_readfirstlane(nref);
                                 if (__all(b == f0 && nref == n0)) {
-                                        hit = leaf_any<true>(static_cast<const RefRec64 *>(sc.refs) + f0, 0, n0, r);
+                                        hit = leaf_any<true>(sc.refs, f0, n0, r, rb);
                                         done = true;
                                 }
                         }
                         if (!done)
-                                hit = leaf_any<kR64>(sc.refs, b, nref, r);
+                                hit = leaf_any<kR64>(sc.refs, b, nref, r, rb);
                 }
                 if (__ballot(hit) != 0ull) {
                         if (hit)
