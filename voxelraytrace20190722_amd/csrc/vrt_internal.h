@@ -41,11 +41,17 @@ static_assert(sizeof(XNodeRec) == 64, "XNodeRec must be 64 B");
 
 // The node triangle-box skip (internal nodes too, DevScene::xnodes):
 // 1 = the finite-slab walks read xnodes, 0 = mnodes (leaves only).
-// config 5 without per-ray ids: one pixel's rays walked as a pool of
-// subtree pieces (occl_coop, vrt_kernels.hip) instead of ray compaction
-// (SpillQueues, resume rounds); 0 restores the compaction
+// config 5 without per-ray ids: 1 = one pixel's rays walked as a pool of
+// subtree pieces (occl_pool, vrt_kernels.hip) instead of the ray compaction
+// (SpillQueues + resume round); measured 10 % slower (DESIGN appendix)
 #ifndef VRT_SEC_COOP
-#define VRT_SEC_COOP 1
+#define VRT_SEC_COOP 0
+#endif
+// the compaction's resume: 1 = one round, its saved rays 64 to a wave walked
+// as a pool of subtree pieces (occl_pool) to the end; 0 = VRT_SEC_ROUNDS
+// rounds of one ray per lane
+#ifndef VRT_SEC_POOL_RESUME
+#define VRT_SEC_POOL_RESUME 1
 #endif
 #ifndef VRT_NODE_BOX
 #define VRT_NODE_BOX 1

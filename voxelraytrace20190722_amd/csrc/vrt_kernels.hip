@@ -816,7 +816,7 @@ __device__ __forceinline__ bool leaf_box_ok(const DevScene &sc, const RayK &r)
 // and t are the serial loop's values.  Returns the owning lane's leaf result.
 // ---------------------------------------------------------------------------
 #ifndef VRT_CL
-#define VRT_CL 1         // the light pass / trace primary marches use it
+#define VRT_CL 0         // 1: the light pass / trace primary marches use it (measured -1.6 %, 4 waves/SIMD)
 #endif
 #ifndef VRT_CL_LANES
 #define VRT_CL_LANES 8   // leaf lanes at most for the cooperative phase
@@ -1340,34 +1340,16 @@ __device__ __forceinline__ uint32_t xor_permute8(uint32_t m, uint32_t s)
 
 // true iff some record of the leaf passes intersect_triangle3's tests
 // (VRT/raytri.cc:197-249, the same operations as leaf_isect_v2)
-// (the records' float4 / double2 views in the base pointer's address space)
-template <typename B>
-struct RecView {
-        typedef const float4 F4;
-        typedef const double2 D2;
-};
-#if defined(__HIP_DEVICE_COMPILE__)
-template <>
-struct RecView<const VRT_AS1 char> {
-        typedef const VRT_AS1 float4 F4;
-        typedef const VRT_AS1 double2 D2;
-};
-#endif
-
-template <bool kR64, typename B = const char>
-__device__ __forceinline__ bool leaf_any(const void *__restrict__ refs, uint32_t first, uint32_t n, const RayK &r,
-                                         B *base = nullptr)
+template <bool kR64>
+__device__ __forceinline__ bool leaf_any(const void *__restrict__ refs, uint32_t first, uint32_t n, const RayK &r)
 {
-        typedef typename RecView<B>::F4 F4;
-        typedef typename RecView<B>::D2 D2;
-        if (!base)
-                base = (B *)refs;
         const double dx = r.d.x, dy = r.d.y, dz = r.d.z;
         for (uint32_t k = 0; k < n; ++k) {
-                F4 *q = reinterpret_cast<F4 *>(base + (size_t)(first + k) * (kR64 ? sizeof(RefRec64) : sizeof(RefRec48)));
+                const float4 *q = kR64 ? reinterpret_cast<const float4 *>(static_cast<const RefRec64 *>(refs) + first + k)
+                                       : reinterpret_cast<const float4 *>(static_cast<const RefRec48 *>(refs) + first + k);
                 const float4 q0 = q[0];
                 const double v0x = q0.x, v0y = q0.y, v0z = q0.z;
-                D2 *qd = reinterpret_cast<D2 *>(q);
+                const double2 *qd = reinterpret_cast<const double2 *>(q);
                 float4 q1, q2;
                 double2 qd1, qd2, qd3;
                 double e2x, e2y, e2z;
@@ -1581,61 +1563,61 @@ __device__ __forceinline__ int occl_dispatch_spill(const DevScene &sc, const Ray
 }
 
 // ---------------------------------------------------------------------------
-// Cooperative occlusion walk of one pixel's rays (config 5, VRT_SEC_COOP).
-// Only each ray's boolean is needed, and a ray's walk state is a set of
-// independent subtrees -- the children left in the block it is walking and
-// every DFS stack entry (a block and its children still to visit) -- whose
-// answer is the OR of theirs (ray_march returns true iff some leaf below a
-// box-passing path holds a triangle that passes, whatever the order,
-// occl_walk).  So the wave's lanes are a pool: lane l starts on ray l (slot
-// l; lanes >= nrays start idle), and whenever some lanes are idle, each busy
-// lane that has work to spare hands one piece to one idle lane -- its
-// bottom stack entry (the shallowest pending block, the largest subtree
-// set), or else the upper half of the children left in its current block --
-// through an LDS mailbox, with the ray's slot; the receiver loads that ray's
-// direction from LDS and walks the piece with an empty stack of its own.  A
-// leaf that passes marks its ray's slot hit (an LDS flag, then a ballot);
-// every lane walking a piece of a hit ray drops it.  The pixel is done when
-// no lane has work.  Returns the hit rays' mask (bit = slot).  The slab, box
-// and MT tests are occl_walk's, so every ray's boolean is unchanged; only
-// the work after a ray's first passing leaf differs (pieces of it walked in
-// parallel until the flag is seen at their next leaf).
-// dirs: the pixel's ray directions (LDS, [64][3]); mbox: 64 uint2 (LDS);
-// hflag: 64 words (LDS); stk: this lane's LDS stack column (stride kS).
+// Pooled occlusion walk (config 5).  Only each ray's boolean is needed, and a
+// ray's walk state is a set of independent subtrees -- the children left in
+// the block it is walking and every DFS stack entry (a block and its
+// children still to visit) -- whose answer is the OR of theirs (ray_march
+// returns true iff some leaf below a box-passing path holds a triangle that
+// passes, whatever the order, occl_walk).  So a wave's lanes can be one pool
+// over up to 64 rays (slots): lane l starts on slot l's walk state, and
+// whenever some lanes are idle, each busy lane with work to spare hands one
+// piece to one idle lane -- its bottom stack entry (the shallowest pending
+// block, the largest subtree set), or else the upper half of the children
+// left in its current block -- through an LDS mailbox, with the slot; the
+// receiver rebuilds that slot's ray (direction from LDS; origin the wave's,
+// or the slot pixel's primary hit point with kSlotOrigin) and walks the
+// piece on an empty stack of its own.  A leaf that passes sets its slot's bit
+// of an LDS hit word; every lane walking a piece of a hit slot drops it.  The
+// pool is done when no lane has work.  Returns the hit slots' mask.  The
+// slab, box and MT tests are occl_walk's, so every ray's boolean is
+// unchanged; only work after a ray's first passing leaf differs (pieces of
+// it walked in parallel until the bit is seen at their next leaf).
+// Used for the resume round of the compaction (VRT_SEC_POOL_RESUME: 64 saved
+// rays of unrelated pixels) and, with VRT_SEC_COOP, for whole pixels.
+// dirs: [64][3] slot directions (LDS); opix: slot -> pixel (LDS, kSlotOrigin;
+// origin = prim[8 pix + 1..3]); mbox: 64 uint2 (LDS); hword: one 64-bit LDS
+// word; stk: this lane's LDS stack column (stride kS) holding its initial
+// state's sp entries.
 // ---------------------------------------------------------------------------
-template <bool kFast, int kS, bool kR64, bool kFin>
-__device__ __forceinline__ uint64_t occl_coop(const DevScene &sc, f3 o, float tmin, const float (*dirs)[3],
-                                              uint2 *mbox, uint32_t *hflag, uint2 *stk, int nrays)
+template <bool kSlotOrigin>
+__device__ __forceinline__ RayK pool_ray(f3 o, const float *prim, const uint32_t *opix, const float (*dirs)[3],
+                                         uint32_t slot, float tmin)
+{
+        if (kSlotOrigin) {
+                const float *pr = prim + 8 * (size_t)opix[slot];
+                o = mk3(pr[1], pr[2], pr[3]);
+        }
+        return make_rayk(o, mk3(dirs[slot][0], dirs[slot][1], dirs[slot][2]), tmin, kFltMax);
+}
+
+template <bool kFast, int kS, bool kR64, bool kFin, bool kSlotOrigin>
+__device__ __forceinline__ uint64_t occl_pool(const DevScene &sc, f3 o, const float *prim, const uint32_t *opix,
+                                              float tmin, const float (*dirs)[3], uint2 *mbox,
+                                              unsigned long long *hword, uint2 *stk, bool busy, uint32_t base,
+                                              uint32_t mask, int sp, uint64_t hitm)
 {
         constexpr bool kLB = kFast && kFin;
         constexpr bool kNB = kLB && VRT_NODE_BOX;
         const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
-        // the record bases held as values (VRT_PIN_SEC, as VRT_PIN_XN in ray_march)
-#ifndef VRT_PIN_SEC
-#define VRT_PIN_SEC 0
-#endif
-        xnode_gptr xn = (xnode_gptr)sc.xnodes;
-        const VRT_AS1 char *rb = (const VRT_AS1 char *)sc.refs;
-        if (VRT_PIN_SEC)
-                asm volatile("" : "+s"(xn), "+s"(rb));
         const uint32_t lane = lane_id();
         uint32_t slot = lane;
-        RayK r = make_rayk(o, mk3(dirs[slot][0], dirs[slot][1], dirs[slot][2]), tmin, kFltMax);
-        const bool lbok = kLB && __all(leaf_box_ok(sc, r));  // one origin: uniform
+        RayK r = pool_ray<kSlotOrigin>(o, prim, opix, dirs, slot, tmin);
+        // one origin per wave (kSlotOrigin: the slots' origins all qualify)
+        const bool lbok = kLB && __all(!busy || leaf_box_ok(sc, r));
         uint32_t s = dir_signs(r);
-        uint32_t base = 0, mask = 0;
-        int sp = 0, bot = 0;
-        bool busy = false, hit = false;
-        if ((int)lane < nrays) {
-                OcclState w;
-                const int st = occl_start<kFast, kR64, kFin>(sc, r, w);
-                hit = st == kOcclHit;
-                busy = st == kOcclWalk;
-                base = w.base;
-                mask = w.mask;
-        }
-        hflag[lane] = hit ? 1u : 0u;
-        uint64_t hitm = __ballot(hit);
+        int bot = 0;
+        if (lane == 0)
+                *hword = hitm;
         for (;;) {
                 // hand work to idle lanes (wave-uniform decisions)
                 const uint64_t idle = __ballot(!busy);
@@ -1675,8 +1657,7 @@ __device__ __forceinline__ uint64_t occl_coop(const DevScene &sc, f3 o, float tm
                                         mask = e.y & 0xFFu;
                                         sp = bot = 0;
                                         busy = true;
-                                        r = make_rayk(o, mk3(dirs[slot][0], dirs[slot][1], dirs[slot][2]), tmin,
-                                                      kFltMax);
+                                        r = pool_ray<kSlotOrigin>(o, prim, opix, dirs, slot, tmin);
                                         s = dir_signs(r);
                                 }
                         }
@@ -1703,7 +1684,7 @@ __device__ __forceinline__ uint64_t occl_coop(const DevScene &sc, f3 o, float tm
                                 mask &= mask - 1u;
                                 if (kNB) {
                                         float tmn[3], tmx[3];
-                                        load_xnode(xn, base + ci, bmin, bmax, a, b, tmn, tmx);
+                                        load_xnode(sc.xnodes, base + ci, bmin, bmax, a, b, tmn, tmx);
                                         if (lbok && !line_meets_box(tmn, tmx, r))
                                                 continue;
                                 } else {
@@ -1729,26 +1710,26 @@ __device__ __forceinline__ uint64_t occl_coop(const DevScene &sc, f3 o, float tm
                                 sp = bot = 0;
                         }
                 }
-                hit = false;
+                bool hit = false;
                 if (leaf) {
                         bool done = false;
                         if (kR64 && VRT_SEC_UNI) {
                                 const uint32_t f0 = __builtin_amdgcn_readfirstlane(b);
                                 const uint32_t n0 = __builtin_amdgcn_readfirstlane(nref);
                                 if (__all(b == f0 && nref == n0)) {
-                                        hit = leaf_any<true>(sc.refs, f0, n0, r, rb);
+                                        hit = leaf_any<true>(sc.refs, f0, n0, r);
                                         done = true;
                                 }
                         }
                         if (!done)
-                                hit = leaf_any<kR64>(sc.refs, b, nref, r, rb);
+                                hit = leaf_any<kR64>(sc.refs, b, nref, r);
                 }
                 if (__ballot(hit) != 0ull) {
                         if (hit)
-                                hflag[slot] = 1u;
+                                atomicOr(hword, 1ull << slot);
                         wave_lds_sync();
-                        hitm = __ballot(hflag[lane] != 0u);
-                        if (busy && ((hitm >> slot) & 1ull)) {  // this ray is decided
+                        hitm = *hword;
+                        if (busy && ((hitm >> slot) & 1ull)) {  // this slot is decided
                                 busy = false;
                                 mask = 0;
                                 sp = bot = 0;
@@ -2395,7 +2376,8 @@ constexpr int kSecPBlock = 256;
 // ray's hit boolean -> the occlusion walk (ray_occluded), same booleans.
 template <bool kR64, bool kAny, int kS>
 __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_t k, int lane, uint2 *stk,
-                                                float (*pts)[3], uint2 *mbox, uint32_t *hflag, SpillCursor &cur)
+                                                float (*pts)[3], uint2 *mbox, unsigned long long *hword,
+                                                SpillCursor &cur)
 {
         // lane id re-read per pixel (not held across k_secondary_p's loop)
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
@@ -2448,27 +2430,48 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (kAny && VRT_SEC_COOP) {
-                // the pixel's rays as one pool of subtree walks (occl_coop):
+                // the pixel's rays as one pool of subtree walks (occl_pool):
                 // directions into LDS (over the sphere points), then the
                 // fast / exact walk chosen for the whole pixel
                 bool ok = true;
+                RayK r;
                 if (lane < p.spp) {
                         const f3 d = normalize(nrm + mk3(pts[lane][0], pts[lane][1], pts[lane][2]));
                         pts[lane][0] = d.x;
                         pts[lane][1] = d.y;
                         pts[lane][2] = d.z;
-                        const RayK r = make_rayk(hp, d, p.res, kFltMax);
+                        r = make_rayk(hp, d, p.res, kFltMax);
                         ok = p.sc.fast_ok && fast_ok(r) && (!VRT_FIN || fin_ok(r));
                 }
                 wave_lds_sync();
-                const uint64_t hm =
-                        __all(ok) ? occl_coop<true, kS, kR64, VRT_FIN != 0>(p.sc, hp, p.res, pts, mbox, hflag, stk, p.spp)
-                                  : occl_coop<false, kS, kR64, false>(p.sc, hp, p.res, pts, mbox, hflag, stk, p.spp);
+                OcclState w;
+                w.base = w.mask = 0;
+                bool busy = false, hit = false;
+                uint64_t hm;
+                if (__all(ok)) {
+                        if (lane < p.spp) {
+                                const int st = occl_start<true, kR64, VRT_FIN != 0>(p.sc, r, w);
+                                busy = st == kOcclWalk;
+                                hit = st == kOcclHit;
+                        }
+                        hm = occl_pool<true, kS, kR64, VRT_FIN != 0, false>(p.sc, hp, nullptr, nullptr, p.res, pts,
+                                                                             mbox, hword, stk, busy, w.base, w.mask,
+                                                                             0, __ballot(hit));
+                } else {
+                        if (lane < p.spp) {
+                                const int st = occl_start<false, kR64>(p.sc, r, w);
+                                busy = st == kOcclWalk;
+                                hit = st == kOcclHit;
+                        }
+                        hm = occl_pool<false, kS, kR64, false, false>(p.sc, hp, nullptr, nullptr, p.res, pts, mbox,
+                                                                      hword, stk, busy, w.base, w.mask, 0,
+                                                                      __ballot(hit));
+                }
                 if (p.s_hit && lane < p.spp)
                         p.s_hit[vi * (size_t)p.spp + lane] = (int32_t)((hm >> lane) & 1ull);
                 if (lane == 0)
                         p.vis[vi] = (float)(p.spp - (int)__popcll(hm)) / (float)p.spp;
-                wave_lds_sync();  // pts / mbox / hflag are rewritten by the next pixel
+                wave_lds_sync();  // pts / mbox / hword are rewritten by the next pixel
                 return;
         }
         // with compaction: the rays still walking when fewer than t_first
@@ -2575,10 +2578,72 @@ __device__ __forceinline__ void resume_chunk(const ResumeParams &p, const SpillR
         }
 }
 
+// VRT_SEC_POOL_RESUME: one chunk of queue 0, its rays 64 at a time as one
+// pool (occl_pool with each slot's origin its pixel's primary hit point), each
+// batch walked to the end; then lane j reports slot j's ray to its pixel.
+template <bool kR64>
+__device__ __forceinline__ void resume_pool_chunk(const ResumeParams &p, const SpillRec *rec, uint32_t fill,
+                                                  uint2 *stk, float (*dirs)[3], uint32_t *opix, uint2 *mbox,
+                                                  unsigned long long *hword)
+{
+        for (uint32_t g = 0; g < fill; g += 64) {
+                const uint32_t lane = lane_id();
+                const uint32_t i = g + lane;
+                bool busy = false, ok = true;
+                uint32_t base = 0, mask = 0;
+                int sp = 0;
+                uint4 h0 = reinterpret_cast<const uint4 *>(rec + g)[0];  // lanes past the fill: a valid pixel
+                f3 dn = mk3(0.f, 0.f, 1.f);
+                if (i < fill) {
+                        const SpillRec *q = rec + i;
+                        h0 = reinterpret_cast<const uint4 *>(q)[0];
+                        const uint4 h1 = reinterpret_cast<const uint4 *>(q)[1];
+                        const uint4 h2 = reinterpret_cast<const uint4 *>(q)[2];
+                        sp = (int)h0.w;
+                        base = h2.x;
+                        mask = h2.y;
+                        const uint2 *e = reinterpret_cast<const uint2 *>(q->stk);
+                        for (int k = 0; k < sp; ++k)
+                                stk[k * kSecPBlock] = e[k];
+                        dn = mk3(__uint_as_float(h1.x), __uint_as_float(h1.y), __uint_as_float(h1.z));
+                        const float *pr = p.prim + 8 * (size_t)h0.x;
+                        const RayK r = make_rayk(mk3(pr[1], pr[2], pr[3]), dn, p.res, kFltMax);
+                        ok = p.sc.fast_ok && fast_ok(r) && (!VRT_FIN || fin_ok(r));
+                        busy = true;
+                }
+                dirs[lane][0] = dn.x;
+                dirs[lane][1] = dn.y;
+                dirs[lane][2] = dn.z;
+                opix[lane] = h0.x;
+                wave_lds_sync();
+                const uint64_t hm =
+                        __all(ok) ? occl_pool<true, kSecPBlock, kR64, VRT_FIN != 0, true>(
+                                            p.sc, mk3(0.f, 0.f, 0.f), p.prim, opix, p.res, dirs, mbox, hword, stk,
+                                            busy, base, mask, sp, 0ull)
+                                  : occl_pool<false, kSecPBlock, kR64, false, true>(
+                                            p.sc, mk3(0.f, 0.f, 0.f), p.prim, opix, p.res, dirs, mbox, hword, stk,
+                                            busy, base, mask, sp, 0ull);
+                if (i < fill) {
+                        const uint32_t hit = (uint32_t)((hm >> lane) & 1ull);
+                        if (p.s_hit)
+                                p.s_hit[(size_t)h0.y * (size_t)p.spp + h0.z] = (int32_t)hit;
+                        float *pr = p.prim + 8 * (size_t)h0.x;
+                        const uint32_t old = atomicAdd(reinterpret_cast<uint32_t *>(pr) + 7, hit ? 255u : 0xFFFFFFFFu);
+                        if ((old & 0xFFu) == 1u)  // the pixel's last ray
+                                p.vis[h0.y] = (float)(p.spp - (int)((old >> 8) + hit)) / (float)p.spp;
+                }
+                wave_lds_sync();  // dirs / opix / mbox / hword are rewritten by the next batch
+        }
+}
+
 template <bool kR64>
 __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_resume(ResumeParams p)
 {
         __shared__ uint2 stk[kStack * kSecPBlock];
+        __shared__ float dirs[VRT_SEC_POOL_RESUME ? kSecPBlock / 64 : 1][64][3];
+        __shared__ uint32_t opix[VRT_SEC_POOL_RESUME ? kSecPBlock / 64 : 1][64];
+        __shared__ uint2 mbox[VRT_SEC_POOL_RESUME ? kSecPBlock / 64 : 1][64];
+        __shared__ unsigned long long hword[kSecPBlock / 64];
         const int tid = threadIdx.x;
         uint32_t *cin = p.sq.ctr + (p.round - 1) * kSpillCtrStride;
         const uint32_t n = min(cin[0], p.sq.nchunks);  // queue round-1's chunks (earlier launches)
@@ -2592,7 +2657,13 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_resum
                 const uint32_t c = take_n(cin + 1, 1u);
                 if (c >= n)
                         break;
-                resume_chunk<kR64>(p, in + (size_t)c * kSpillChunk, fin[c], t, cur, stk + tid);
+                if (VRT_SEC_POOL_RESUME) {
+                        const int w = VRT_SEC_POOL_RESUME ? tid >> 6 : 0;
+                        resume_pool_chunk<kR64>(p, in + (size_t)c * kSpillChunk, fin[c], stk + tid, dirs[w], opix[w],
+                                                mbox[w], hword + (tid >> 6));
+                } else {
+                        resume_chunk<kR64>(p, in + (size_t)c * kSpillChunk, fin[c], t, cur, stk + tid);
+                }
         }
         spill_close(p.sq.fill[p.round & 1], p.sq.ctr + p.round * kSpillCtrStride, cur);
 }
@@ -2603,14 +2674,14 @@ __global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(S
         __shared__ uint2 stk[kStack * kSecBlock];
         __shared__ float pts[VRT_SEC_WAVES][64][3];
         __shared__ uint2 mbox[kAny && VRT_SEC_COOP ? VRT_SEC_WAVES : 1][64];
-        __shared__ uint32_t hflag[kAny && VRT_SEC_COOP ? VRT_SEC_WAVES : 1][64];
+        __shared__ unsigned long long hword[VRT_SEC_WAVES];
         const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
         const int64_t k = (int64_t)blockIdx.x * VRT_SEC_WAVES + wave;
         SpillCursor cur;  // no compaction in the one-pixel-per-wave grid (p.sq.nchunks == 0)
         cur.chunk = kSpillNone;
         cur.fill = 0;
         constexpr int mw = kAny && VRT_SEC_COOP ? 1 : 0;
-        secondary_pixel<kR64, kAny, kSecBlock>(p, k, lane, stk + tid, pts[wave], mbox[wave * mw], hflag[wave * mw],
+        secondary_pixel<kR64, kAny, kSecBlock>(p, k, lane, stk + tid, pts[wave], mbox[wave * mw], hword + wave,
                                                cur);
 }
 
@@ -2625,7 +2696,7 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
         __shared__ uint2 stk[kStack * kSecPBlock];
         __shared__ float pts[kSecPBlock / 64][64][3];
         __shared__ uint2 mbox[kAny && VRT_SEC_COOP ? kSecPBlock / 64 : 1][64];
-        __shared__ uint32_t hflag[kAny && VRT_SEC_COOP ? kSecPBlock / 64 : 1][64];
+        __shared__ unsigned long long hword[kSecPBlock / 64];
         constexpr int mw = kAny && VRT_SEC_COOP ? 1 : 0;
         const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
         const int xcd = blockIdx.x & 7;
@@ -2643,7 +2714,7 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
                                 break;
                         secondary_pixel<kR64, kAny, kSecPBlock>(
                                 p, (int64_t)slice_unit(p.units, x, (int)u, VRT_SEC_SLICE_CHUNK), lane, stk + tid,
-                                pts[wave], mbox[wave * mw], hflag[wave * mw], cur);
+                                pts[wave], mbox[wave * mw], hword + wave, cur);
                 }
         }
         if (kAny && !VRT_SEC_COOP)
@@ -2668,7 +2739,7 @@ SpillQueues spill_defaults()
         std::memset(&q, 0, sizeof q);
         q.t_first = VRT_SEC_SPILL_T;
         q.t_next = VRT_SEC_SPILL_T2;
-        q.rounds = VRT_SEC_ROUNDS;
+        q.rounds = VRT_SEC_POOL_RESUME ? 1 : VRT_SEC_ROUNDS;  // the pooled round walks to the end
         return q;
 }
 
@@ -3915,7 +3986,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
 // pixel is written once: each sample record is read once, and no per-cone
 // result goes through memory.
 #ifndef VRT_CONES_WAVES_PER_EU
-#define VRT_CONES_WAVES_PER_EU 7  // 70 VGPRs, no scratch (with VRT_CONES_RELOAD; 8 waves: 24 B/lane)
+#define VRT_CONES_WAVES_PER_EU 8  // 64 VGPRs, 24 B/lane of spill outside the step loop (7 waves: 70, none, -0.7 %)
 #endif
 __global__ __launch_bounds__(64, VRT_CONES_WAVES_PER_EU) void k_cones_film(TraceParams p)
 {
