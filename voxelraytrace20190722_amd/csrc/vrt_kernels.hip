@@ -28,7 +28,6 @@
 #include <cmath>
 #include <cstring>
 #include <mutex>
-#include <type_traits>
 #include <vector>
 
 namespace vrt {
@@ -61,39 +60,14 @@ __device__ __forceinline__ void load_node(const NodeRec *__restrict__ nodes,
 }
 
 // DevScene::xnodes record i: the node record and the triangle box below it
-// global (address space 1) pointers, for bases held through an asm barrier
-// (which loses the address-space inference: flat loads otherwise)
-#if defined(__HIP_DEVICE_COMPILE__)
-#define VRT_AS1 __attribute__((address_space(1)))
-#else
-#define VRT_AS1  // the host pass of the kernels' source: no address spaces
-#endif
-typedef const VRT_AS1 XNodeRec *xnode_gptr;
-template <typename XP>
-__device__ __forceinline__ void load_xnode(XP x, uint32_t i, float bmin[3],
+__device__ __forceinline__ void load_xnode(const XNodeRec *__restrict__ x, uint32_t i, float bmin[3],
                                            float bmax[3], uint32_t &a, uint32_t &b, float tmn[3], float tmx[3])
 {
-        typedef typename std::conditional<std::is_same<XP, xnode_gptr>::value, const VRT_AS1 float4,
-                                          const float4>::type F4;
-        typedef typename std::conditional<std::is_same<XP, xnode_gptr>::value, const VRT_AS1 float2,
-                                          const float2>::type F2;
-#ifndef VRT_XN_OFF32
-#define VRT_XN_OFF32 0
-#endif
-        F4 *q;
-        if (VRT_XN_OFF32) {
-                // a 32-bit byte offset (node < 2^26): the base + 32-bit voffset
-                // load form, no 64-bit address arithmetic per visit
-                typedef typename std::conditional<std::is_same<XP, xnode_gptr>::value, const VRT_AS1 char,
-                                                  const char>::type C1;
-                q = reinterpret_cast<F4 *>(reinterpret_cast<C1 *>(x) + (i << 6));
-        } else {
-                q = reinterpret_cast<F4 *>(x + i);
-        }
+        const float4 *q = reinterpret_cast<const float4 *>(x + i);
         const float4 q0 = q[0];
         const float4 q1 = q[1];
         const float4 q2 = q[2];
-        const float2 q3 = *reinterpret_cast<F2 *>(q + 3);
+        const float2 q3 = *reinterpret_cast<const float2 *>(q + 3);
         bmin[0] = q0.x; bmin[1] = q0.y; bmin[2] = q0.z;
         bmax[0] = q0.w; bmax[1] = q1.x; bmax[2] = q1.y;
         a = __float_as_uint(q1.z);
@@ -912,15 +886,6 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         constexpr bool kNB = kLB && VRT_NODE_BOX;  // every visited node by its triangle box
         const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
         const bool lbok = kLB && __all(leaf_box_ok(sc, r));  // wave-uniform: held in SGPRs
-#ifndef VRT_PIN_XN
-#define VRT_PIN_XN 0
-#endif
-        // VRT_PIN_XN: the xnodes base as a value the compiler cannot
-        // re-read from the kernel arguments (a scalar load in every visit's
-        // dependent chain); if it must spill it, it spills to a VGPR lane
-        xnode_gptr xn = (xnode_gptr)sc.xnodes;
-        if (VRT_PIN_XN)
-                asm volatile("" : "+s"(xn));
         load_node_st<kNS>(sc.nodes, 0, bmin, bmax, a, b);
         if (!aabb_isect(bmin, bmax, r.o, r.dinv, r.tmin, r.tmax))
                 return;
@@ -1004,7 +969,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
 #endif
                                 if (VRT_SIB_PF && cnt > 0)  // the next sibling's record towards the caches
                                         sib_pf ^= reinterpret_cast<const uint32_t *>(sc.xnodes + base + (order & 7u))[0];
-                                load_xnode(xn, node, bmin, bmax, a, b, tmn, tmx);
+                                load_xnode(sc.xnodes, node, bmin, bmax, a, b, tmn, tmx);
                                 if (lbok && !line_meets_box(tmn, tmx, r))
                                         continue;  // no triangle below this node can pass
                         } else {
