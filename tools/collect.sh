@@ -16,4 +16,5 @@ exec bash tools/check_call.sh "$@" \
   "reh8|200|$B --no-cpu --no-pmc --rehearse-ranks 8 --steps 256" \
   "reh4|200|$B --no-cpu --no-pmc --rehearse-ranks 4 --steps 256" \
   "reh2|200|$B --no-cpu --no-pmc --rehearse-ranks 2 --steps 256" \
-  "gloo2|300|$B --no-cpu --no-pmc --gpus 2 --dist-backend gloo"
+  "gloo2|300|$B --no-cpu --no-pmc --gpus 2 --dist-backend gloo" \
+  "abim8|200|$B --abi-multi --abi-multi-virtual 8 --steps 64"
