@@ -123,6 +123,22 @@ __device__ __forceinline__ void load_node_st(const NodeRec *__restrict__ nodes, 
 #ifndef VRT_PHASE_STAMPS
 #define VRT_PHASE_STAMPS 0
 #endif
+// bit ci of m -> bit ci ^ s (children renumbered so that ascending order is
+// the ray's direction-sign order)
+__device__ __forceinline__ uint32_t xor_permute8(uint32_t m, uint32_t s)
+{
+        m = (s & 4u) ? (((m & 0x0Fu) << 4) | ((m >> 4) & 0x0Fu)) : m;
+        m = (s & 2u) ? (((m & 0x33u) << 2) | ((m >> 2) & 0x33u)) : m;
+        m = (s & 1u) ? (((m & 0x55u) << 1) | ((m >> 1) & 0x55u)) : m;
+        return m;
+}
+
+// children in ascending (ci ^ s): the near half of each axis first
+__device__ __forceinline__ uint32_t dir_signs(const RayK &r)
+{
+        return (r.d.x < 0.f ? 4u : 0u) | (r.d.y < 0.f ? 2u : 0u) | (r.d.z < 0.f ? 1u : 0u);
+}
+
 // wave reductions (every lane of the wave active)
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 {
@@ -976,6 +992,18 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                 load_node_st<kNS>(nodes, node, bmin, bmax, a, b);
                         }
                         if (!(a & kLeafBit)) {
+#ifndef VRT_PRED_PF
+#define VRT_PRED_PF 0
+#endif
+                                if (VRT_PRED_PF && kNB) {
+                                        // the child most likely visited next (the first child
+                                        // with content in direction-sign order) towards the
+                                        // caches while this node is expanded
+                                        const uint32_t sg = dir_signs(r), pm = xor_permute8(b & 0xFFu, sg);
+                                        if (pm)
+                                                sib_pf ^= reinterpret_cast<const uint32_t *>(
+                                                        sc.xnodes + a + ((uint32_t)__builtin_ctz(pm) ^ sg))[0];
+                                }
                                 if (cnt) {
                                         stk[sp * kS] = make_uint2(base, order | ((uint32_t)cnt << 24));
                                         if (kCount)
@@ -1132,7 +1160,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 }
         }
 #endif
-        if (VRT_SIB_PF)
+        if (VRT_SIB_PF || VRT_PRED_PF)
                 asm volatile("" : : "v"(sib_pf));
         if (kCount) {
                 // 1 root test + 8 per expanded node, minus the children the
@@ -1293,16 +1321,6 @@ __device__ __forceinline__ uint32_t child_hit_mask(const float bmin[3], const fl
         return hm;
 }
 
-// bit ci of m -> bit ci ^ s (children renumbered so that ascending order is
-// the ray's direction-sign order)
-__device__ __forceinline__ uint32_t xor_permute8(uint32_t m, uint32_t s)
-{
-        m = (s & 4u) ? (((m & 0x0Fu) << 4) | ((m >> 4) & 0x0Fu)) : m;
-        m = (s & 2u) ? (((m & 0x33u) << 2) | ((m >> 2) & 0x33u)) : m;
-        m = (s & 1u) ? (((m & 0x55u) << 1) | ((m >> 1) & 0x55u)) : m;
-        return m;
-}
-
 // true iff some record of the leaf passes intersect_triangle3's tests
 // (VRT/raytri.cc:197-249, the same operations as leaf_isect_v2)
 template <bool kR64>
@@ -1363,12 +1381,6 @@ struct OcclState {
         int sp;
 };
 enum { kOcclMiss = 0, kOcclHit = 1, kOcclSpill = 2, kOcclWalk = 3 };
-
-// children in ascending (ci ^ s): the near half of each axis first
-__device__ __forceinline__ uint32_t dir_signs(const RayK &r)
-{
-        return (r.d.x < 0.f ? 4u : 0u) | (r.d.y < 0.f ? 2u : 0u) | (r.d.z < 0.f ? 1u : 0u);
-}
 
 // The root: kOcclMiss / kOcclHit when it decides the ray (its box missed, or
 // a leaf root), else kOcclWalk with w = the root's hit children.
