@@ -270,6 +270,10 @@ int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
  * runs the n-rank frame on a one-GPU box.  Handles created without it are
  * unaffected. */
 #define VRT_TEST_VIRTUAL_RANKS 8
+/* VRT_TEST_STREAM_LEFTOVER makes config-5's streaming resume round leave
+ * every odd chunk of saved rays to its batch-pool launch (the path a chunk
+ * with a degenerate ray takes). */
+#define VRT_TEST_STREAM_LEFTOVER 16
 #define VRT_TEST_VIRTUAL_RANKS_N(n) (VRT_TEST_VIRTUAL_RANKS | ((n) << 8))
 int vrt_set_test_flags(int flags);
 

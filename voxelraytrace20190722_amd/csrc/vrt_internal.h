@@ -261,6 +261,7 @@ struct SpillQueues {
         uint32_t t_first;    // phase-A threshold (walking lanes)
         uint32_t t_next;     // threshold of resume rounds 1..rounds-1
         int32_t rounds;      // resume launches
+        int32_t stream;      // the resume round streams its rays (VRT_SEC_STREAM; films < 2^26 pixels)
 };
 
 // Tile deal of a multi-rank frame.  The ntx x nty grid of

@@ -2502,6 +2502,8 @@ struct ResumeParams {
         int32_t spp;
         float res;
         int32_t round;
+        int32_t nx, W8;  // pixel index <-> primary record index (VRT_SEC_STREAM)
+        int32_t test_flags;
         SpillQueues sq;
 };
 
@@ -2613,6 +2615,305 @@ __device__ __forceinline__ void resume_pool_chunk(const ResumeParams &p, const S
         }
 }
 
+
+// ---------------------------------------------------------------------------
+// VRT_SEC_STREAM: the resume round as one stream per wave.  The wave's lanes
+// are a pool over 64 slots (as occl_pool), but a slot whose ray has ended is
+// refilled at once with the next saved ray of the queue (chunks taken with
+// take_n), so lanes idle only when no piece can be handed over AND the
+// queue is empty -- the batch pool instead waits for its 64 rays' longest
+// walk before taking the next 64.  Per iteration: idle lanes first take
+// pieces handed over by busy lanes (bottom stack entry, or the upper half of
+// the children left); idle lanes left over take new rays into free slots;
+// every busy lane advances to its next leaf and tests it; a passing leaf
+// sets its slot's bit of the LDS hit word (pieces of hit slots drop); then a
+// slot that no lane still walks (a wave OR of the busy lanes' slot bits) has
+// ended, and lane j reports slot j's ray to its pixel (hits << 8 | rays out,
+// as the batch path) and frees the slot.  A chunk not wholly on the fast
+// walk (a degenerate direction, an origin far from the scene) is appended
+// to a list (queue 1's fill array, count at ctr[3]) that a batch-pool launch
+// after this one works through (k_sec_resume, leftover mode).
+// LDS per wave: dirs [64][3], sinfo [64] = primary record index | sample <<
+// 26 (the host uses this path only for films under 2^26 pixels), mbox [64]
+// (also the free-slot map), the hit word.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_or_u64(uint64_t v)
+{
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+                v |= (uint64_t)__shfl_xor((long long)v, o, 64);
+        return v;
+}
+
+template <bool kR64>
+__device__ __forceinline__ bool stream_chunk_fast(const ResumeParams &p, const SpillRec *rec, uint32_t fill,
+                                                  uint32_t c)
+{
+        const uint32_t lane = lane_id();
+        bool ok = !((p.test_flags & VRT_TEST_STREAM_LEFTOVER) && (c & 1u));  // test hook: odd chunks left over
+        for (uint32_t i = lane; i < fill; i += 64) {
+                const uint4 h0 = reinterpret_cast<const uint4 *>(rec + i)[0];
+                const uint4 h1 = reinterpret_cast<const uint4 *>(rec + i)[1];
+                const float *pr = p.prim + 8 * (size_t)h0.x;
+                const RayK r = make_rayk(mk3(pr[1], pr[2], pr[3]),
+                                         mk3(__uint_as_float(h1.x), __uint_as_float(h1.y), __uint_as_float(h1.z)),
+                                         p.res, kFltMax);
+                ok = ok && p.sc.fast_ok && fast_ok(r) && (!VRT_FIN || fin_ok(r)) && (!VRT_FIN || leaf_box_ok(p.sc, r));
+        }
+        return __all(ok);
+}
+
+template <bool kR64>
+__device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *cin, uint32_t nch,
+                                              const uint32_t *fins, const SpillRec *in, uint2 *stk,
+                                              float (*dirs)[3], uint32_t *sinfo, uint2 *mbox,
+                                              unsigned long long *hword)
+{
+        constexpr bool kFin = VRT_FIN != 0;
+        constexpr bool kNB = kFin && VRT_NODE_BOX;
+        const DevScene &sc = p.sc;
+        const NodeRec *__restrict__ nodes = kFin ? sc.mnodes : sc.nodes;
+        const uint32_t lane = lane_id();
+        const uint64_t lt = (1ull << lane) - 1ull;
+        uint64_t assigned = 0;  // wave-uniform: slots holding a ray
+        uint32_t chunk = 0, cur = 0, fill = 0;
+        bool more = true;  // wave-uniform: chunks may remain in the queue
+        bool busy = false;
+        uint32_t slot = lane, base = 0, mask = 0, s = 0;
+        int sp = 0, bot = 0;
+        RayK r;
+        r.o = r.d = r.dinv = mk3(0.f, 0.f, 0.f);
+        r.tmin = p.res;
+        r.tmax = kFltMax;
+        if (lane == 0)
+                *hword = 0ull;
+        wave_lds_sync();
+        for (;;) {
+                // 1. hand pieces to idle lanes
+                uint64_t idle = __ballot(!busy);
+                const bool spare = busy && (sp > bot || __popc(mask) >= 2);
+                const uint64_t don = __ballot(spare);
+                uint32_t given = 0;
+                if (idle != 0ull && don != 0ull) {
+                        given = min((uint32_t)__popcll(idle), (uint32_t)__popcll(don));
+                        if (spare) {
+                                const uint32_t k = (uint32_t)__popcll(don & lt);
+                                if (k < given) {
+                                        uint2 e;
+                                        if (sp > bot) {
+                                                e = stk[bot * kSecPBlock];
+                                                ++bot;
+                                        } else {
+                                                uint32_t give = mask;
+                                                for (int c = (__popc(mask) + 1) >> 1; c > 0; --c)
+                                                        give &= give - 1u;
+                                                mask ^= give;
+                                                e = make_uint2(base, give);
+                                        }
+                                        mbox[k] = make_uint2(e.x, e.y | (slot << 8));
+                                }
+                        }
+                        wave_lds_sync();
+                        if (!busy) {
+                                const uint32_t k = (uint32_t)__popcll(idle & lt);
+                                if (k < given) {
+                                        const uint2 e = mbox[k];
+                                        slot = e.y >> 8;
+                                        base = e.x;
+                                        mask = e.y & 0xFFu;
+                                        sp = bot = 0;
+                                        busy = true;
+                                        const float *pr = p.prim + 8 * (size_t)(sinfo[slot] & 0x3FFFFFFu);
+                                        r = make_rayk(mk3(pr[1], pr[2], pr[3]),
+                                                      mk3(dirs[slot][0], dirs[slot][1], dirs[slot][2]), p.res,
+                                                      kFltMax);
+                                        s = dir_signs(r);
+                                }
+                        }
+                        wave_lds_sync();
+                }
+                // 2. idle lanes left over take new rays into free slots
+                uint32_t left = (uint32_t)__popcll(idle) - given;
+                if (left > 0 && more) {
+                        if (cur >= fill) {
+                                const uint32_t c = take_n(cin + 1, 1u);
+                                if (c >= nch) {
+                                        more = false;
+                                } else {
+                                        const uint32_t f = __builtin_amdgcn_readfirstlane(fins[c]);
+                                        if (stream_chunk_fast<kR64>(p, in + (size_t)c * kSpillChunk, f, c)) {
+                                                chunk = c;
+                                                cur = 0;
+                                                fill = f;
+                                        } else {
+                                                // left to the batch pool's launch after this one
+                                                const uint32_t j = take_n(p.sq.ctr + 3, 1u);
+                                                if (lane == 0)
+                                                        p.sq.fill[1][j] = c;
+                                        }
+                                }
+                        }
+                        if (more && cur < fill) {
+                                const uint64_t freem = ~assigned;
+                                const uint32_t ntake = min(min(left, (uint32_t)__popcll(freem)), fill - cur);
+                                const bool fr = (freem >> lane) & 1ull;
+                                const uint32_t rank = (uint32_t)__popcll(freem & lt);
+                                const uint64_t taken = __ballot(fr && rank < ntake);
+                                uint32_t *map = reinterpret_cast<uint32_t *>(mbox);
+                                if (fr && rank < ntake)
+                                        map[rank] = lane;
+                                wave_lds_sync();
+                                const uint64_t still = __ballot(!busy);
+                                if (!busy) {
+                                        const uint32_t k = (uint32_t)__popcll(still & lt);
+                                        if (k < ntake) {
+                                                slot = map[k];
+                                                const SpillRec *q = in + (size_t)chunk * kSpillChunk + cur + k;
+                                                const uint4 h0 = reinterpret_cast<const uint4 *>(q)[0];
+                                                const uint4 h1 = reinterpret_cast<const uint4 *>(q)[1];
+                                                const uint4 h2 = reinterpret_cast<const uint4 *>(q)[2];
+                                                sp = (int)h0.w;
+                                                bot = 0;
+                                                base = h2.x;
+                                                mask = h2.y;
+                                                const uint2 *e = reinterpret_cast<const uint2 *>(q->stk);
+                                                for (int j = 0; j < sp; ++j)
+                                                        stk[j * kSecPBlock] = e[j];
+                                                const f3 d = mk3(__uint_as_float(h1.x), __uint_as_float(h1.y),
+                                                                 __uint_as_float(h1.z));
+                                                dirs[slot][0] = d.x;
+                                                dirs[slot][1] = d.y;
+                                                dirs[slot][2] = d.z;
+                                                sinfo[slot] = h0.x | (h0.z << 26);
+                                                const float *pr = p.prim + 8 * (size_t)h0.x;
+                                                r = make_rayk(mk3(pr[1], pr[2], pr[3]), d, p.res, kFltMax);
+                                                s = dir_signs(r);
+                                                busy = true;
+                                        }
+                                }
+                                assigned |= taken;
+                                cur += ntake;
+                                if (lane == 0)
+                                        *hword &= ~taken;
+                                wave_lds_sync();
+                        }
+                }
+                if (__ballot(busy) == 0ull) {
+                        if (!more)
+                                break;
+                        if (cur >= fill)
+                                continue;  // take the next chunk
+                }
+                // 3. every busy lane: advance to its next leaf and test it (occl_walk)
+                bool leaf = false;
+                uint32_t nref = 0, b = 0;
+                if (busy) {
+                        float bmin[3], bmax[3];
+                        uint32_t a;
+                        for (;;) {
+                                if (mask == 0) {
+                                        if (sp == bot)
+                                                break;
+                                        --sp;
+                                        const uint2 e = stk[sp * kSecPBlock];
+                                        base = e.x;
+                                        mask = e.y;
+                                        if (!VRT_POP_VISIT)
+                                                continue;
+                                }
+                                const uint32_t ci = (uint32_t)__builtin_ctz(mask) ^ s;
+                                mask &= mask - 1u;
+                                if (kNB) {
+                                        float tmn[3], tmx[3];
+                                        load_xnode(sc.xnodes, base + ci, bmin, bmax, a, b, tmn, tmx);
+                                        if (!line_meets_box(tmn, tmx, r))
+                                                continue;
+                                } else {
+                                        load_node(nodes, base + ci, bmin, bmax, a, b);
+                                }
+                                if (!(a & kLeafBit)) {
+                                        if (mask) {
+                                                stk[sp * kSecPBlock] = make_uint2(base, mask);
+                                                ++sp;
+                                        }
+                                        mask = xor_permute8(child_hit_mask<true, kFin>(bmin, bmax, r) & b, s);
+                                        base = a;
+                                        continue;
+                                }
+                                nref = a & ~kLeafBit;
+                                if (kFin && !kNB && !line_meets_box(bmin, bmax, r))
+                                        continue;
+                                leaf = true;
+                                break;
+                        }
+                        if (!leaf) {
+                                busy = false;
+                                sp = bot = 0;
+                        }
+                }
+                bool hit = false;
+                if (leaf) {
+                        bool done = false;
+                        if (kR64 && VRT_SEC_UNI) {
+                                const uint32_t f0 = __builtin_amdgcn_readfirstlane(b);
+                                const uint32_t n0 = __builtin_amdgcn_readfirstlane(nref);
+                                if (__all(b == f0 && nref == n0)) {
+                                        hit = leaf_any<true>(sc.refs, f0, n0, r);
+                                        done = true;
+                                }
+                        }
+                        if (!done)
+                                hit = leaf_any<kR64>(sc.refs, b, nref, r);
+                }
+                if (__ballot(hit) != 0ull) {
+                        if (hit)
+                                atomicOr(hword, 1ull << slot);
+                        wave_lds_sync();
+                        const uint64_t hm = *hword;
+                        if (busy && ((hm >> slot) & 1ull)) {
+                                busy = false;
+                                mask = 0;
+                                sp = bot = 0;
+                        }
+                }
+                // 4. slots no lane walks any more have ended: report and free them
+                const uint64_t live = wave_or_u64(busy ? 1ull << slot : 0ull);
+                const uint64_t done = assigned & ~live;
+                if (done != 0ull) {
+                        const uint64_t hm = *hword;
+                        if ((done >> lane) & 1ull) {
+                                const uint32_t inf = sinfo[lane];
+                                const uint32_t pix = inf & 0x3FFFFFFu, smp = inf >> 26;
+                                const uint32_t vi = (pix / (uint32_t)p.W8) * (uint32_t)p.nx + pix % (uint32_t)p.W8;
+                                const uint32_t h = (uint32_t)((hm >> lane) & 1ull);
+                                if (p.s_hit)
+                                        p.s_hit[(size_t)vi * (size_t)p.spp + smp] = (int32_t)h;
+                                float *pr = p.prim + 8 * (size_t)pix;
+                                const uint32_t old = atomicAdd(reinterpret_cast<uint32_t *>(pr) + 7, h ? 255u : 0xFFFFFFFFu);
+                                if ((old & 0xFFu) == 1u)  // the pixel's last ray
+                                        p.vis[vi] = (float)(p.spp - (int)((old >> 8) + h)) / (float)p.spp;
+                        }
+                        assigned &= ~done;
+                }
+        }
+}
+
+// The streaming resume round (VRT_SEC_STREAM, films under 2^26 pixels): one
+// resident generation, each wave one stream (resume_stream) over queue 0.
+template <bool kR64>
+__global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_stream(ResumeParams p)
+{
+        __shared__ uint2 stk[kStack * kSecPBlock];
+        __shared__ float dirs[kSecPBlock / 64][64][3];
+        __shared__ uint32_t sinfo[kSecPBlock / 64][64];
+        __shared__ uint2 mbox[kSecPBlock / 64][64];
+        __shared__ unsigned long long hword[kSecPBlock / 64];
+        const int tid = threadIdx.x, w = tid >> 6;
+        uint32_t *cin = p.sq.ctr;
+        const uint32_t n = min(cin[0], p.sq.nchunks);
+        resume_stream<kR64>(p, cin, n, p.sq.fill[0], p.sq.rec[0], stk + tid, dirs[w], sinfo[w], mbox[w], hword + w);
+}
+
 template <bool kR64>
 __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_resume(ResumeParams p)
 {
@@ -2630,10 +2931,21 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_resum
         SpillCursor cur;
         cur.chunk = kSpillNone;
         cur.fill = 0;
+        // leftover mode (after k_sec_stream): the chunks it listed, from ctr[4]
+        const bool left = VRT_SEC_POOL_RESUME && p.sq.stream;
+        const uint32_t nl = left ? p.sq.ctr[3] : 0u;
         for (;;) {
-                const uint32_t c = take_n(cin + 1, 1u);
-                if (c >= n)
-                        break;
+                uint32_t c;
+                if (left) {
+                        const uint32_t j = take_n(p.sq.ctr + 4, 1u);
+                        if (j >= nl)
+                                break;
+                        c = __builtin_amdgcn_readfirstlane(p.sq.fill[1][j]);
+                } else {
+                        c = take_n(cin + 1, 1u);
+                        if (c >= n)
+                                break;
+                }
                 if (VRT_SEC_POOL_RESUME) {
                         const int w = VRT_SEC_POOL_RESUME ? tid >> 6 : 0;
                         resume_pool_chunk<kR64>(p, in + (size_t)c * kSpillChunk, fin[c], stk + tid, dirs[w], opix[w],
@@ -2717,6 +3029,7 @@ SpillQueues spill_defaults()
         q.t_first = VRT_SEC_SPILL_T;
         q.t_next = VRT_SEC_SPILL_T2;
         q.rounds = VRT_SEC_POOL_RESUME ? 1 : VRT_SEC_ROUNDS;  // the pooled round walks to the end
+        q.stream = 0;  // set per launch (launch_secondary: films under 2^26 pixels)
         return q;
 }
 
@@ -2791,11 +3104,28 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                         rp2.s_hit = s_hit;
                         rp2.spp = spp;
                         rp2.res = res;
+                        rp2.nx = rp.cam.nx;
+                        rp2.test_flags = rp.test_flags;
+                        rp2.W8 = rp.ntx * 8;
                         rp2.sq = sp.sq;
-                        for (int r = 1; r <= sp.sq.rounds; ++r) {
-                                rp2.round = r;
-                                hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(g),
+                        rp2.sq.stream = (int64_t)rp.ntx * 8 * rp.nty * 8 < (1 << 26) ? 1 : 0;
+#ifndef VRT_SEC_STREAM
+#define VRT_SEC_STREAM 1
+#endif
+                        rp2.sq.stream = VRT_SEC_POOL_RESUME && VRT_SEC_STREAM && rp2.sq.stream;
+                        if (rp2.sq.stream) {
+                                rp2.round = 1;
+                                hipLaunchKernelGGL(w ? k_sec_stream<true> : k_sec_stream<false>, dim3(g),
                                                    dim3(kSecPBlock), 0, st, rp2);
+                                // the chunks the stream left (normally none): a small batch-pool launch
+                                hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(8),
+                                                   dim3(kSecPBlock), 0, st, rp2);
+                        } else {
+                                for (int r = 1; r <= sp.sq.rounds; ++r) {
+                                        rp2.round = r;
+                                        hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(g),
+                                                           dim3(kSecPBlock), 0, st, rp2);
+                                }
                         }
                 }
                 return hipGetLastError();
