@@ -371,6 +371,19 @@ int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam,
                             int nranks, int image_layout, float *d_out,
                             void *stream);
 
+/* The whole reference main() frame (VRT/main.cc:75-126) in one call: the
+ * light pass + cone_trace_init_filter (as vrt_lightmap_build, on the scene's
+ * stream) and, beside them on `stream`, the view's primary march, which reads
+ * no light map; the cone-traced shading then waits for the filter.  Values
+ * equal vrt_lightmap_build followed by vrt_render_trace_device (same tile
+ * deal / layout arguments).  Returns after one host sync (the light pass's
+ * hit count, *hits, may be NULL); the image is complete in stream order. */
+int vrt_trace_frame_device(vrt_scene *s, const vrt_camera *light_cam,
+                           const vrt_film *light_film, const vrt_camera *cam,
+                           const vrt_film *film, float min_voxel, int rank,
+                           int nranks, int image_layout, float *d_out,
+                           void *stream, int64_t *hits);
+
 /* ---- output (VRT/stb_image_write.h:178,723-757) ------------------------- */
 /* Byte-identical to stbi_write_hdr: returns 1 on success, 0 on failure. */
 int vrt_write_hdr(const char *filename, int w, int h, int comp,

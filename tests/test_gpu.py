@@ -531,6 +531,51 @@ def test_trace_device_tiles_reassemble(proxy_small):
     assert np.array_equal(bits(img.cpu().numpy().reshape(40, 48, 3)), bits(direct))
 
 
+def test_trace_frame_one_call_matches_two_calls_and_oracle(proxy_small):
+    """vrt_trace_frame_device (light map + filter beside the view's primary
+    march, then the cones) equals vrt_lightmap_build + vrt_render_trace_device
+    and the oracle, bit for bit: a whole-image frame, then 3 ranks' tile
+    shares re-assembled, then frames queued back to back on one stream with
+    alternating views (the next frame's light pass waits for the previous
+    frame's cones, which read the light map)."""
+    import torch
+    tree = vrt.VoxelOctree(proxy_small, 6)
+    osc = po.Scene(proxy_small, 6)
+    lfilm = vrt.Film(1, 1, 96, 96)
+    ohits = osc.lightmap(po.camera(*LIGHT), 1.0, 1.0, 96, 96, nthreads=8)
+    res = tree.min_voxel(6)
+    mn, mx = tree.root_box
+    views = [(vrt.to_radian(90), (1.0, 1.3, -0.2), (0.0, 0.4, 0.0), (0.0, 1.0, 0.0)), vrt.sweep_pose(mn, mx, 5, 16)]
+    film = vrt.Film(1, 1, 48, 40)
+    want = [osc.render_trace(po.camera(*v), 1.0, 1.0, 48, 40, res, nthreads=8, samples=False) for v in views]
+    st = torch.cuda.Stream()
+    img = torch.zeros((40, 48, 3), device="cuda")
+    hits = tree.trace_frame_device(vrt.Camera(*LIGHT), lfilm, vrt.Camera(*views[0]), film, 0, 1, 1, img.data_ptr(),
+                                   res, st.cuda_stream)
+    st.synchronize()
+    assert hits == ohits > 0
+    assert np.array_equal(bits(img.cpu().numpy()), bits(want[0]))
+    assert np.array_equal(bits(tree.render_trace(vrt.Camera(*views[0]), film, res)), bits(want[0]))
+    n = 3
+    tpr = vrt.tiles_per_rank(film, n)
+    g = torch.zeros(n * tpr * 192, device="cuda")
+    for r in range(n):
+        tree.trace_frame_device(vrt.Camera(*LIGHT), lfilm, vrt.Camera(*views[1]), film, r, n, 0,
+                                g[r * tpr * 192:].data_ptr(), res, st.cuda_stream)
+    full = torch.zeros(48 * 40 * 3, device="cuda")
+    st.synchronize()
+    vrt.unpack_tiles_device(film, n, g.data_ptr(), full.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(full.cpu().numpy().reshape(40, 48, 3)), bits(want[1]))
+    outs = [torch.zeros((40, 48, 3), device="cuda") for _ in range(6)]
+    for k, o in enumerate(outs):
+        tree.trace_frame_device(vrt.Camera(*LIGHT), lfilm, vrt.Camera(*views[k % 2]), film, 0, 1, 1, o.data_ptr(),
+                                res, st.cuda_stream)
+    st.synchronize()
+    for k, o in enumerate(outs):
+        assert np.array_equal(bits(o.cpu().numpy()), bits(want[k % 2])), k
+
+
 # ---- GPU octree build (SURVEY §8 row f3) ----
 @pytest.mark.parametrize("depth", [1, 2, 5, 8, 9])
 def test_device_build_equals_host_build(proxy_small, depth):

@@ -141,6 +141,8 @@ SIGNATURES = {
     "vrt_render_trace": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), C.c_float, f32p, i32p, f32p]),
     "vrt_render_trace_device": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), C.c_float, C.c_int, C.c_int,
                                           C.c_int, _P, _P]),
+    "vrt_trace_frame_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float,
+                                         C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]),
     "vrt_obj_load": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_P)]),
     "vrt_obj_free": (None, [_P]),
     "vrt_obj_info": (C.c_int, [_P, C.POINTER(ObjInfo)]),

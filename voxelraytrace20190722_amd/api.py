@@ -477,6 +477,19 @@ class VoxelOctree:
                                             None if stream_ptr is None else C.c_void_p(stream_ptr)),
               "vrt_render_trace_device")
 
+    def trace_frame_device(self, light_cam, light_film, cam, film, rank, nranks, image_layout, d_out_ptr,
+                           min_voxel=0.0, stream_ptr=None):
+        """The reference main() frame in one call (vrt_trace_frame_device):
+        light map + filter beside the view's primary march, then the cones;
+        returns the light pass's hit count."""
+        hits = C.c_int64()
+        check(lib().vrt_trace_frame_device(self.h, C.byref(light_cam.c), C.byref(light_film.c), C.byref(cam.c),
+                                           C.byref(film.c), float(min_voxel), int(rank), int(nranks),
+                                           int(image_layout), C.c_void_p(d_out_ptr),
+                                           None if stream_ptr is None else C.c_void_p(stream_ptr), C.byref(hits)),
+              "vrt_trace_frame_device")
+        return hits.value
+
 
 class MultiOctree:
     """The octree replicated on every device of a mask, with an RCCL

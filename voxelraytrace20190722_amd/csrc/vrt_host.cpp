@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -376,6 +377,7 @@ struct vrt_scene {
         // scene-owned device scratch (light map, split-trace records): the
         // event of the last launch that used it
         hipEvent_t scratch_ev = nullptr;
+        hipEvent_t lm_ev = nullptr;    // vrt_trace_frame_device: the light map is filtered
         bool scratch_live = false;
         // vrt_render's host-output path (render_to_host): a device image kept
         // between calls, its pinned host staging copy, a second render stream
@@ -1038,6 +1040,8 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                                 (void)hipEventDestroy(s->q_ev[k]);
                 if (s->scratch_ev)
                         (void)hipEventDestroy(s->scratch_ev);
+                if (s->lm_ev)
+                        (void)hipEventDestroy(s->lm_ev);
                 HostOut &ho = s->ho;
                 if (ho.st2)
                         (void)hipStreamSynchronize(ho.st2);
@@ -1868,17 +1872,14 @@ static hipError_t ensure_light_scratch(vrt_scene *s, size_t bytes)
         return e;
 }
 
-extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
-                                  const vrt_film *light_film, int64_t *hits)
+// The light pass + filter of VRT/main.cc:75-100 on the scene's stream
+// (caller holds s->mu).  `overlap` (may be empty) is called right after the
+// light pass is enqueued, before the one mid-build host sync, so work it
+// enqueues on another stream runs beside the light pass; on return the
+// filter is enqueued and *lm_done (if given) recorded after it.
+static int lightmap_enqueue(vrt_scene *s, const vrt_camera *light_cam, const vrt_film *light_film,
+                            unsigned int *hits, const std::function<int()> &overlap, hipEvent_t lm_done)
 {
-        if (s && need_device(s))
-                return VRT_E_NODEVICE;
-        if (!s || !light_cam)
-                return fail(VRT_E_INVALID, "null argument");
-        if (int rc = film_ok(light_film))
-                return rc;
-        std::lock_guard<std::mutex> lk(s->mu);
-        HIPCHK(hipSetDevice(s->device));
         const int64_t nnodes = (int64_t)s->nodes.size();
         const int ptx = light_film->nx / 8, pty = light_film->ny / 8;
         const int64_t ns = (int64_t)64 * ptx * pty * 4;
@@ -1935,6 +1936,9 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         lp.samp = samp;
         HIPCHK(hipEventRecord(s->ev0, s->stream));
         HIPCHK(launch_light(lp, s->stream));
+        if (overlap)
+                if (int rc = overlap())
+                        return rc;
         // the sort takes its length on the host: the one mid-build sync
         unsigned int nhit = 0;
         HIPCHK(hipMemcpyAsync(&nhit, d_count, sizeof nhit, hipMemcpyDeviceToHost, s->stream));
@@ -1950,13 +1954,33 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
                 HIPCHK(launch_lm_level(s->dev.nodes, s->level_begin[l - 1], s->level_begin[l], s->d_lm, s->stream));
         HIPCHK(launch_lm_aux(s->dev.nodes, s->d_lm, nnodes, d_cc, d_bad, s->stream));
         HIPCHK(hipEventRecord(s->ev1, s->stream));
+        if (lm_done)
+                HIPCHK(hipEventRecord(lm_done, s->stream));
         s->timed = true;
+        s->lm_ready = true;
+        *hits = nhit;
+        return VRT_OK;
+}
+
+extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
+                                  const vrt_film *light_film, int64_t *hits)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !light_cam)
+                return fail(VRT_E_INVALID, "null argument");
+        if (int rc = film_ok(light_film))
+                return rc;
+        std::lock_guard<std::mutex> lk(s->mu);
+        HIPCHK(hipSetDevice(s->device));
+        unsigned int nhit = 0;
+        if (int rc = lightmap_enqueue(s, light_cam, light_film, &nhit, {}, nullptr))
+                return rc;
         if (int rc = scratch_release(s, s->stream))
                 return rc;
         HIPCHK(hipStreamSynchronize(s->stream));
         if (hits)
                 *hits = (int64_t)nhit;
-        s->lm_ready = true;
         return VRT_OK;
 }
 
@@ -2137,6 +2161,66 @@ extern "C" int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam, cons
         if (int rc = scratch_release(s, st))
                 return rc;
         s->timed = true;
+        return VRT_OK;
+}
+
+// The reference main() frame in one call (VRT/main.cc:75-126): light pass
+// + filter on the scene's stream and, beside them on `stream`, the view's
+// primary march (k_trace_prim reads no light map); the cones + film pass
+// waits for the filter.  Same values as vrt_lightmap_build followed by
+// vrt_render_trace_device.  Returns once the filter is enqueued (the light
+// pass's hit count needs one host sync); the image is ordered on `stream`.
+extern "C" int vrt_trace_frame_device(vrt_scene *s, const vrt_camera *light_cam, const vrt_film *light_film,
+                                      const vrt_camera *cam, const vrt_film *film, float min_voxel, int rank,
+                                      int nranks, int image_layout, float *d_out, void *stream, int64_t *hits)
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !light_cam || !cam || !d_out)
+                return fail(VRT_E_INVALID, "null argument");
+        if (int rc = film_ok(light_film))
+                return rc;
+        if (int rc = film_ok(film))
+                return rc;
+        if (nranks < 1 || rank < 0 || rank >= nranks)
+                return fail(VRT_E_INVALID, "rank %d of %d", rank, nranks);
+        if (image_layout && nranks != 1)
+                return fail(VRT_E_INVALID, "image_layout requires nranks == 1");
+        if (int rc = trace_ok(s, min_voxel))
+                return rc;
+        std::lock_guard<std::mutex> lk(s->mu);
+        HIPCHK(hipSetDevice(s->device));
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        if (!s->lm_ev)
+                HIPCHK(hipEventCreateWithFlags(&s->lm_ev, hipEventDisableTiming));
+        if (!s->d_lm)  // the trace parameters point into the light-map block
+                HIPCHK(hipMalloc(reinterpret_cast<void **>(&s->d_lm),
+                                 s->nodes.size() * (sizeof(LMRec) + sizeof(float4)) + 256));
+        TraceParams tp0, tp;
+        fill_trace_params(s, cam, film, min_voxel, rank, nranks, &tp0);
+        tp0.r.image_layout = image_layout;
+        tp0.r.out = d_out;
+        if (int rc = trace_scratch(s, tp0, &tp, st))
+                return rc;
+        if (!tp.rec)
+                return fail(VRT_E_INVALID, "vrt_trace_frame_device needs the split trace (VRT_TRACE_FUSED unset)");
+        unsigned int nhit = 0;
+        auto overlap = [&]() -> int {
+                // the view's primary march beside the light pass (its records
+                // wait only for the previous frame's users of the scratch)
+                if (int rc = scratch_acquire(s, st))
+                        return rc;
+                HIPCHK(launch_trace_prim(tp, st));
+                return VRT_OK;
+        };
+        if (int rc = lightmap_enqueue(s, light_cam, light_film, &nhit, overlap, s->lm_ev))
+                return rc;
+        HIPCHK(hipStreamWaitEvent(st, s->lm_ev, 0));
+        HIPCHK(launch_cones(tp, st));
+        if (int rc = scratch_release(s, st))
+                return rc;
+        if (hits)
+                *hits = (int64_t)nhit;
         return VRT_OK;
 }
 

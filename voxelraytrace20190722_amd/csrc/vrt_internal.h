@@ -536,6 +536,8 @@ hipError_t launch_lm_accum(int64_t n, const uint64_t *keys_sorted, const uint32_
 hipError_t launch_lm_leaves(const NodeRec *nodes, int64_t nnodes, LMRec *lm, hipStream_t st);
 hipError_t launch_lm_level(const NodeRec *nodes, int64_t begin, int64_t end, LMRec *lm, hipStream_t st);
 hipError_t launch_trace(const TraceParams &p, hipStream_t st);
+hipError_t launch_trace_prim(const TraceParams &p, hipStream_t st);
+hipError_t launch_cones(const TraceParams &p, hipStream_t st);
 // per-node cone-descent records and the light map's finiteness flag
 hipError_t launch_lm_aux(const NodeRec *nodes, const LMRec *lm, int64_t n, float4 *cc, uint32_t *bad,
                          hipStream_t st);

@@ -792,100 +792,12 @@ __device__ __forceinline__ bool leaf_box_ok(const DevScene &sc, const RayK &r)
                fabsf(r.o.z - sc.lb_center[2]) <= sc.lb_reach;
 }
 
-// ---------------------------------------------------------------------------
-// Cooperative leaf phase (kCL, the light pass and the trace render's primary
-// march over large-leaf scenes): when only a few lanes of a full wave hold a
-// leaf (the tail of long walks -- near-vertical light rays test up to ~2,500
-// triangles over a few dozen leaves), the whole wave tests each such leaf's
-// records for that lane's ray, 64 records at a time, and reduces them to
-// ray_march_isect's answer: the first strict minimum of depth in record order
-// (VRT/voxel_octree.cc:122-125) = the smallest (depth, record index), depth
-// >= +0 ordered by its bits.  A NaN depth as some lane's first hit (the only
-// way a NaN can be the serial answer) sends that leaf to the serial loop.
-// The winning record is re-run by the owning lane (any = false), so tri, u, v
-// and t are the serial loop's values.  Returns the owning lane's leaf result.
-// ---------------------------------------------------------------------------
-#ifndef VRT_CL
-#define VRT_CL 0         // 1: the light pass / trace primary marches use it (measured -1.6 %, 4 waves/SIMD)
-#endif
-#ifndef VRT_CL_LANES
-#define VRT_CL_LANES 8   // leaf lanes at most for the cooperative phase
-#endif
-#ifndef VRT_CL_RATIO
-#define VRT_CL_RATIO 4   // ... and the longest leaf >= this x their number (records)
-#endif
-
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
-{
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-                const uint64_t w = (uint64_t)__shfl_xor((long long)v, o, 64);
-                v = w < v ? w : v;
-        }
-        return v;
-}
-
-template <bool kR64>
-__device__ __forceinline__ bool coop_leaves(const DevScene &sc, const RayK &r, uint64_t lm, uint32_t first,
-                                            uint32_t nref, MarchResult &m)
-{
-        const uint32_t lane = lane_id();
-        bool mine = false;
-        while (lm) {  // wave-uniform
-                const int L = __builtin_ctzll(lm);
-                lm &= lm - 1ull;
-                const uint32_t f = __builtin_amdgcn_readlane(first, L);
-                const uint32_t n = __builtin_amdgcn_readlane(nref, L);
-                RayK rl;
-                rl.o.x = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.o.x), L));
-                rl.o.y = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.o.y), L));
-                rl.o.z = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.o.z), L));
-                rl.d.x = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.d.x), L));
-                rl.d.y = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.d.y), L));
-                rl.d.z = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(r.d.z), L));
-                bool any = false;
-                float best = 0.f, bt = 0.f;
-                uint32_t kb = 0;
-                MarchResult mm;
-                for (uint32_t k = lane; k < n; k += 64) {
-                        const float4 *q = kR64 ? reinterpret_cast<const float4 *>(static_cast<const RefRec64 *>(sc.refs) + f + k)
-                                               : reinterpret_cast<const float4 *>(static_cast<const RefRec48 *>(sc.refs) + f + k);
-                        const double2 *qd = reinterpret_cast<const double2 *>(q);
-                        const float4 q0 = q[0];
-                        float4 q1 = q0, q2 = q0;
-                        double2 qd1 = {}, qd2 = {}, qd3 = {};
-                        if (kR64) {
-                                qd1 = qd[1];
-                                qd2 = qd[2];
-                                qd3 = qd[3];
-                        } else {
-                                q1 = q[1];
-                                q2 = q[2];
-                        }
-                        if (mt_record<kR64>(q0, q1, q2, qd1, qd2, qd3, rl, any, best, bt, mm))
-                                kb = k;
-                }
-                if (__ballot(any && isnan(best)) != 0ull) {
-                        if ((int)lane == L)  // the serial loop decides this leaf
-                                mine = leaf_isect_v2<false, kR64>(sc.refs, first, nref, r, m);
-                        continue;
-                }
-                const uint64_t key = any ? ((uint64_t)__float_as_uint(best) << 32) | kb : ~0ull;
-                const uint64_t kmin = wave_min_u64(key);
-                if (kmin != ~0ull && (int)lane == L) {
-                        // the winner again, as the serial loop's taking step
-                        mine = leaf_isect_v2<false, kR64>(sc.refs, first + (uint32_t)kmin, 1u, r, m);
-                }
-        }
-        return mine;
-}
-
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).  The finite-slab fast walk (kStd == 2)
 // reads DevScene::mnodes and skips a leaf whose triangles' box the ray's
 // line misses (no triangle of it can pass; the leaf is left as the reference
 // leaves it, with no record).
-template <bool kCount, bool kFast, int kS, int kStd, bool kUni, bool kR64, int kNS = 0, bool kCL = false>
+template <bool kCount, bool kFast, int kS, int kStd, bool kUni, bool kR64, int kNS = 0>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint2 *stk,
                                           uint32_t *stk_aux,
@@ -932,11 +844,6 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         uint32_t d_it = 0, d_lp = 0, d_tri = 0, d_lpmax = 0, d_lpsum = 0, d_phmax = 0;
         unsigned long long d_tin = 0, d_tleaf = 0;
 #endif
-        // kCL: lanes stay in the loop when their walk ends (done), so that
-        // the whole wave can take part in a cooperative leaf phase
-        const bool cl_full = kCL && __ballot(1) == ~0ull;
-        bool done = false;
-        uint32_t sib_pf = 0;  // VRT_SIB_PF: the prefetches' words, kept live
         for (;;) {
                 bool leaf = false;
                 uint32_t node = 0, nref = 0;
@@ -947,8 +854,6 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
 #define VRT_POP_VISIT 1
 #endif
                 for (;;) {
-                        if (kCL && done)
-                                break;
 #if VRT_PHASE_STAMPS
                         ++d_it;
 #endif
@@ -980,11 +885,6 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                 path_rem[depth * kS] = 7u - ((fpos >> (3 * ci)) & 7u);
                         if (kNB) {
                                 float tmn[3], tmx[3];
-#ifndef VRT_SIB_PF
-#define VRT_SIB_PF 0
-#endif
-                                if (VRT_SIB_PF && cnt > 0)  // the next sibling's record towards the caches
-                                        sib_pf ^= reinterpret_cast<const uint32_t *>(sc.xnodes + base + (order & 7u))[0];
                                 load_xnode(sc.xnodes, node, bmin, bmax, a, b, tmn, tmx);
                                 if (lbok && !line_meets_box(tmn, tmx, r))
                                         continue;  // no triangle below this node can pass
@@ -992,18 +892,6 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                 load_node_st<kNS>(nodes, node, bmin, bmax, a, b);
                         }
                         if (!(a & kLeafBit)) {
-#ifndef VRT_PRED_PF
-#define VRT_PRED_PF 0
-#endif
-                                if (VRT_PRED_PF && kNB) {
-                                        // the child most likely visited next (the first child
-                                        // with content in direction-sign order) towards the
-                                        // caches while this node is expanded
-                                        const uint32_t sg = dir_signs(r), pm = xor_permute8(b & 0xFFu, sg);
-                                        if (pm)
-                                                sib_pf ^= reinterpret_cast<const uint32_t *>(
-                                                        sc.xnodes + a + ((uint32_t)__builtin_ctz(pm) ^ sg))[0];
-                                }
                                 if (cnt) {
                                         stk[sp * kS] = make_uint2(base, order | ((uint32_t)cnt << 24));
                                         if (kCount)
@@ -1043,27 +931,6 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         d_phmax += d_lpmax;
                 }
 #endif
-                if (kCL) {
-                        done = done || !leaf;
-                        if (__ballot(!done) == 0ull)
-                                break;
-                        const uint64_t lm = __ballot(leaf);
-                        const uint32_t nl = (uint32_t)__popcll(lm);
-                        bool coop = cl_full && nl <= VRT_CL_LANES;
-                        if (coop)
-                                coop = wave_max_u32(leaf ? nref : 0u) >= (uint32_t)VRT_CL_RATIO * nl;
-                        bool lh = false;
-                        if (coop)
-                                lh = coop_leaves<kR64>(sc, r, lm, b, nref, m);
-                        else if (leaf)
-                                lh = leaf_isect<kCount, kUni, kR64>(sc, b, nref, r, m);
-                        if (leaf && lh) {
-                                m.hit = true;
-                                m.node = node;
-                                done = true;
-                        }
-                        continue;
-                }
                 if (!leaf)
                         break;
 #if VRT_PHASE_STAMPS
@@ -1160,8 +1027,6 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 }
         }
 #endif
-        if (VRT_SIB_PF || VRT_PRED_PF)
-                asm volatile("" : : "v"(sib_pf));
         if (kCount) {
                 // 1 root test + 8 per expanded node, minus the children the
                 // reference never popped on the path it stopped on.
@@ -1211,7 +1076,7 @@ __device__ __forceinline__ bool fin_ok(const RayK &r)
                fabsf(r.dinv.z) <= 0x1p64f;
 }
 
-template <bool kCount, int kS, bool kUni, bool kR64, int kNS = 0, bool kCL = false>
+template <bool kCount, int kS, bool kUni, bool kR64, int kNS = 0>
 __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const RayK &r,
                                                    uint2 *sb, uint32_t *sa, uint32_t *pr,
                                                    MarchResult &m)
@@ -1221,7 +1086,7 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
 #endif
         if (__all(sc.fast_ok && fast_ok(r))) {
                 if (VRT_FIN && !kCount && __all(fin_ok(r)))
-                        ray_march<kCount, true, kS, 2, kUni, kR64, kNS, kCL>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, 2, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
                 else if (!VRT_FIN && VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
                         ray_march<kCount, true, kS, 1, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
                 else
@@ -1902,22 +1767,12 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         ty += p.ty0;
         // pixel, sample and Camera::gen_rays4 direction (VRT/camera.cc:95-112)
         // of lane l
-#ifndef VRT_UNIT_ROWS
-#define VRT_UNIT_ROWS 0
-#endif
         auto sample_of = [&](int l, int &px, int &py, int &s, int &lx, int &ly) {
                 s = l & 3;
                 const int pix = l >> 2;
-                if (VRT_UNIT_ROWS) {
-                        // unit = 2 whole tile rows (8x2 pixels): each row's 8
-                        // pixels are 96 B = three whole 32-B sectors of the film
-                        lx = pix & 7;
-                        ly = wave * 2 + (pix >> 3);
-                } else {
-                        // unit = a 4x4 quadrant of the tile
-                        lx = (wave & 1) * 4 + (pix & 3);
-                        ly = (wave >> 1) * 4 + (pix >> 2);
-                }
+                // unit = a 4x4 quadrant of the tile
+                lx = (wave & 1) * 4 + (pix & 3);
+                ly = (wave >> 1) * 4 + (pix >> 2);
                 px = tx * 8 + lx;
                 py = ty * 8 + ly;
                 // opaque per unit, as the deal's sizes above: the film size and
@@ -3655,7 +3510,7 @@ __device__ __forceinline__ void light_unit(const LightParams &p, uint2 *stk, int
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock, true, kR64, 0, VRT_CL>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         if (!m.hit)
                 return;
         // canonical order: render_mt task t = tx*8 + ty (VRT/camera.h:50-56)
@@ -4200,7 +4055,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock, true, kR64, 0, VRT_CL>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         f3 col;
         if (m.hit) {
                 f3 nrm;
@@ -4258,16 +4113,19 @@ __device__ __forceinline__ void trace_prim_unit(const TraceParams &p, uint2 *stk
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
                                  dn, c.tmin, c.tmax);
         MarchResult m;
-        ray_march_dispatch<false, kRenderBlock, true, kR64, 0, VRT_CL>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
+        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
         float4 *o = p.rec + 4 * slot;
         if (m.hit) {
                 f3 nrm;
                 const f3 albedo = hit_albedo(p.r.sc, m, nrm);
-                const f3 direct = compute_illum(p.lm, m.node, -r.d);
+                // the hit leaf and -d: the direct term compute_illum(leaf, -d)
+                // is taken in k_cones_film, so this pass never reads the light
+                // map and can run while the light map is being built
+                const f3 nd = -r.d;
                 o[0] = make_float4(m.hp.x, m.hp.y, m.hp.z, 1.f);
                 o[1] = make_float4(nrm.x, nrm.y, nrm.z, 0.f);
                 o[2] = make_float4(albedo.x, albedo.y, albedo.z, 0.f);
-                o[3] = make_float4(direct.x, direct.y, direct.z, 0.f);
+                o[3] = make_float4(__uint_as_float(m.node), nd.x, nd.y, nd.z);
         } else {
                 const f3 sk = sky(r.d.y);
                 o[0] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -4319,7 +4177,8 @@ __global__ __launch_bounds__(64, VRT_CONES_WAVES_PER_EU) void k_cones_film(Trace
                         diffuse = cone_trace_isect(p, mk3(r0.x, r0.y, r0.z), mk3(r1.x, r1.y, r1.z));
                 }
                 const float4 r2 = p.rec[4 * slot + 2], r3 = p.rec[4 * slot + 3];
-                const f3 lsum = diffuse + mk3(r3.x, r3.y, r3.z);
+                const f3 direct = compute_illum(p.lm, __float_as_uint(r3.x), mk3(r3.y, r3.z, r3.w));
+                const f3 lsum = diffuse + direct;
                 col = mk3(r2.x * lsum.x, r2.y * lsum.y, r2.z * lsum.z);
         } else {
                 const float4 r2 = p.rec[4 * slot + 2];
@@ -4416,9 +4275,27 @@ hipError_t launch_trace(const TraceParams &p, hipStream_t st)
                 hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace<true> : k_trace<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
                 return hipGetLastError();
         }
-        const int64_t nslots = (int64_t)p.r.tiles_this_rank * 256;
+        if (hipError_t e = launch_trace_prim(p, st))
+                return e;
+        return launch_cones(p, st);
+}
+
+// the split trace's two halves: the primary march (no light-map read) and
+// the cones + film pass (reads the light map)
+hipError_t launch_trace_prim(const TraceParams &p, hipStream_t st)
+{
+        if (p.r.tiles_this_rank <= 0)
+                return hipSuccess;
         hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace_prim<true> : k_trace_prim<false>,
                            dim3(trace_vblocks(p.r.tiles_this_rank)), dim3(kRenderBlock), 0, st, p);
+        return hipGetLastError();
+}
+
+hipError_t launch_cones(const TraceParams &p, hipStream_t st)
+{
+        if (p.r.tiles_this_rank <= 0)
+                return hipSuccess;
+        const int64_t nslots = (int64_t)p.r.tiles_this_rank * 256;
         hipLaunchKernelGGL(k_cones_film, dim3((unsigned)(nslots / 64)), dim3(64), 0, st, p);
         return hipGetLastError();
 }
