@@ -163,7 +163,8 @@ def run_pmc(a, save_dir=""):
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     child = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-counters", "--no-pmc", "--no-d9",
-             "--frames-in-flight", "1", "--frames-in-flight-secondary", "1", "--warmup", "0", "--steps",
+             "--frames-in-flight", "1", "--frames-in-flight-secondary", "1", "--frames-in-flight-trace", "1",
+             "--warmup", "0", "--steps",
              str(a.steps), *workload_args(a)]
     per, nd, meta, child_ms, skipped = {}, {}, {}, {}, []
     stats = None
@@ -395,6 +396,9 @@ def parse():
                         "unpacks; from 4 ranks on the deal gives it fewer tiles than the others)")
     p.add_argument("--rehearse-render-only", action="store_true",
                    help="with --rehearse-ranks: time the share's renders alone (no gather, no unpack)")
+    p.add_argument("--frames-in-flight-trace", type=int, default=2,
+                   help="frames in flight for --mode trace: the scene keeps two light-map / record sets, so a "
+                        "frame's light pass runs beside the previous frame's cone-traced shading")
     p.add_argument("--frames-in-flight-secondary", type=int, default=1,
                    help="frames in flight for --mode secondary (round 4, streaming resume round: 1 / 2 / 3 in "
                         "flight 17.81 / 17.85 / 18.08 ms per frame)")
@@ -623,7 +627,7 @@ def main():
     # buffers, so frame k+1's persistent grid fills the CUs while frame k's
     # last (latency-bound) units finish -- a launch's ramp-down is ~0.2 ms
     # whatever its size.  Every frame is still one full launch.
-    nfl = 1 if (trace or a.dist_backend == "gloo") else max(1, a.frames_in_flight)
+    nfl = 1 if a.dist_backend == "gloo" else max(1, a.frames_in_flight_trace if trace else a.frames_in_flight)
     if a.mode == "secondary" and a.frames_in_flight_secondary is not None:
         nfl = max(1, a.frames_in_flight_secondary)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nfl - 1)]

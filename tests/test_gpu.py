@@ -537,7 +537,9 @@ def test_trace_frame_one_call_matches_two_calls_and_oracle(proxy_small):
     and the oracle, bit for bit: a whole-image frame, then 3 ranks' tile
     shares re-assembled, then frames queued back to back on one stream with
     alternating views (the next frame's light pass waits for the previous
-    frame's cones, which read the light map)."""
+    frame's cones, which read the light map), on two streams (frames in
+    flight over the scene's two light-map / record sets), then the separate
+    light-map build and render again."""
     import torch
     tree = vrt.VoxelOctree(proxy_small, 6)
     osc = po.Scene(proxy_small, 6)
@@ -568,12 +570,15 @@ def test_trace_frame_one_call_matches_two_calls_and_oracle(proxy_small):
     torch.cuda.synchronize()
     assert np.array_equal(bits(full.cpu().numpy().reshape(40, 48, 3)), bits(want[1]))
     outs = [torch.zeros((40, 48, 3), device="cuda") for _ in range(6)]
+    sts = [st, torch.cuda.Stream()]  # frames in flight: the two light-map sets alternate
     for k, o in enumerate(outs):
         tree.trace_frame_device(vrt.Camera(*LIGHT), lfilm, vrt.Camera(*views[k % 2]), film, 0, 1, 1, o.data_ptr(),
-                                res, st.cuda_stream)
-    st.synchronize()
+                                res, sts[k % 2].cuda_stream)
+    torch.cuda.synchronize()
     for k, o in enumerate(outs):
         assert np.array_equal(bits(o.cpu().numpy()), bits(want[k % 2])), k
+    assert tree.lightmap(vrt.Camera(*LIGHT), lfilm) == ohits
+    assert np.array_equal(bits(tree.render_trace(vrt.Camera(*views[1]), film, res)), bits(want[1]))
 
 
 # ---- GPU octree build ----

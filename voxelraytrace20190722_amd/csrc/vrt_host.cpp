@@ -326,6 +326,15 @@ struct HostOut {
         hipEvent_t ev_j = nullptr;  // second render stream joined back
 };
 
+// One set of the full trace's scene scratch (vrt_scene::ts).
+struct TraceSet {
+        LMRec *lm = nullptr;  // nodes x (LMRec + float4 cone record) + the finiteness flag
+        void *rec = nullptr;  // split-trace records (64 B per sample)
+        size_t rec_bytes = 0;
+        hipEvent_t ev = nullptr;  // its last user's work
+        bool live = false;
+};
+
 struct vrt_scene {
         int device = 0;
         int max_depth = 0;
@@ -343,13 +352,18 @@ struct vrt_scene {
         int64_t tex_bytes = 0;
         vrt_scene_info_t info{};
         std::vector<int64_t> level_begin;  // BFS level l (1-based) = [lb[l-1], lb[l])
-        // full trace: per-node light map + light-pass scratch (device)
-        LMRec *d_lm = nullptr;
-        bool lm_ready = false;
+        // full trace: two sets of {light-map block (LMRec + cone-descent
+        // records + finiteness flag), split-trace records}, taken by
+        // alternate light-map builds so that one frame's cone-traced shading
+        // runs beside the next frame's light pass; each with the event of its
+        // last user.  lm_cur = the set with the latest light map (-1: none).
+        // The light pass's own scratch (keys, sort) is used on the scene
+        // stream only.
+        TraceSet ts[2];
+        int ts_next = 0;
+        int lm_cur = -1;
         void *d_light = nullptr;
         size_t light_bytes = 0;
-        void *d_trace = nullptr;  // split-trace scratch (records + colours)
-        size_t trace_bytes = 0;
         // config-5 ray compaction (SpillQueues): round counters + two record
         // queues of spill_cap chunks each; two sets, used by alternate
         // frames (two config-5 frames in flight on two streams), each with
@@ -374,11 +388,7 @@ struct vrt_scene {
         hipEvent_t q_ev[kQueueSlots] = {};
         bool q_live[kQueueSlots] = {};
         int q_next = 0;
-        // scene-owned device scratch (light map, split-trace records): the
-        // event of the last launch that used it
-        hipEvent_t scratch_ev = nullptr;
-        hipEvent_t lm_ev = nullptr;    // vrt_trace_frame_device: the light map is filtered
-        bool scratch_live = false;
+        hipEvent_t lm_ev = nullptr;  // vrt_trace_frame_device: the light map is filtered
         // vrt_render's host-output path (render_to_host): a device image kept
         // between calls, its pinned host staging copy, a second render stream
         // and a copy stream, and an event per band
@@ -849,7 +859,8 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         HIPCHK(hipEventCreate(&s->ev1));
         for (int k = 0; k < kQueueSlots; ++k)
                 HIPCHK(hipEventCreateWithFlags(&s->q_ev[k], hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&s->scratch_ev, hipEventDisableTiming));
+        for (TraceSet &t : s->ts)
+                HIPCHK(hipEventCreateWithFlags(&t.ev, hipEventDisableTiming));
         return VRT_OK;
 }
 
@@ -1011,20 +1022,24 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
 {
         if (!s)
                 return;
-        if (s->d_mem || s->d_lm || s->d_light || s->d_trace || s->d_spill[0] || s->d_spill[1] || s->stream || s->ev0 ||
-            s->ev1 ||
-            s->scratch_ev) {
+        if (s->d_mem || s->ts[0].lm || s->ts[1].lm || s->d_light || s->ts[0].rec || s->ts[1].rec || s->d_spill[0] ||
+            s->d_spill[1] || s->stream || s->ev0 || s->ev1 || s->ts[0].ev || s->ts[1].ev) {
                 (void)hipSetDevice(s->device);
                 if (s->stream)
                         (void)hipStreamSynchronize(s->stream);
                 if (s->d_mem)
                         (void)hipFree(s->d_mem);
-                if (s->d_lm)
-                        (void)hipFree(s->d_lm);
+                (void)hipDeviceSynchronize();  // trace frames run on callers' streams too
+                for (TraceSet &t : s->ts) {
+                        if (t.lm)
+                                (void)hipFree(t.lm);
+                        if (t.rec)
+                                (void)hipFree(t.rec);
+                        if (t.ev)
+                                (void)hipEventDestroy(t.ev);
+                }
                 if (s->d_light)
                         (void)hipFree(s->d_light);
-                if (s->d_trace)
-                        (void)hipFree(s->d_trace);
                 for (int k = 0; k < 2; ++k) {
                         if (s->d_spill[k])
                                 (void)hipFree(s->d_spill[k]);
@@ -1038,8 +1053,6 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                 for (int k = 0; k < kQueueSlots; ++k)
                         if (s->q_ev[k])
                                 (void)hipEventDestroy(s->q_ev[k]);
-                if (s->scratch_ev)
-                        (void)hipEventDestroy(s->scratch_ev);
                 if (s->lm_ev)
                         (void)hipEventDestroy(s->lm_ev);
                 HostOut &ho = s->ho;
@@ -1284,8 +1297,8 @@ static int render_launch(vrt_scene *s, RenderParams &p, bool instrumented, hipSt
         return VRT_OK;
 }
 
-static int scratch_acquire(vrt_scene *s, hipStream_t st);
-static int scratch_release(vrt_scene *s, hipStream_t st);
+static int ts_acquire(vrt_scene *s, int i, hipStream_t st);
+static int ts_release(vrt_scene *s, int i, hipStream_t st);
 
 // Compaction queues of one config-5 launch (SpillQueues): room
 // for every secondary ray of this rank, in chunks, up to kSpillCapMax records
@@ -1380,20 +1393,28 @@ static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int ra
         return VRT_OK;
 }
 
-// Scene-owned scratch (light map, split-trace records) serves one launch at
-// a time: the next user's stream waits for the previous user's (caller
-// holds s->mu).
-static int scratch_acquire(vrt_scene *s, hipStream_t st)
+// A trace scratch set (vrt_scene::ts) serves one user at a time: the next
+// user's stream waits for the previous user's (caller holds s->mu).
+static int ts_acquire(vrt_scene *s, int i, hipStream_t st)
 {
-        if (s->scratch_live)
-                HIPCHK(hipStreamWaitEvent(st, s->scratch_ev, 0));
+        if (s->ts[i].live)
+                HIPCHK(hipStreamWaitEvent(st, s->ts[i].ev, 0));
         return VRT_OK;
 }
 
-static int scratch_release(vrt_scene *s, hipStream_t st)
+static int ts_release(vrt_scene *s, int i, hipStream_t st)
 {
-        HIPCHK(hipEventRecord(s->scratch_ev, st));
-        s->scratch_live = true;
+        HIPCHK(hipEventRecord(s->ts[i].ev, st));
+        s->ts[i].live = true;
+        return VRT_OK;
+}
+
+// set i's light-map block (nodes x (LMRec + float4) + the flag word)
+static int ensure_lm(vrt_scene *s, int i)
+{
+        if (!s->ts[i].lm)
+                HIPCHK(hipMalloc(reinterpret_cast<void **>(&s->ts[i].lm),
+                                 s->nodes.size() * (sizeof(LMRec) + sizeof(float4)) + 256));
         return VRT_OK;
 }
 
@@ -1877,7 +1898,7 @@ static hipError_t ensure_light_scratch(vrt_scene *s, size_t bytes)
 // light pass is enqueued, before the one mid-build host sync, so work it
 // enqueues on another stream runs beside the light pass; on return the
 // filter is enqueued and *lm_done (if given) recorded after it.
-static int lightmap_enqueue(vrt_scene *s, const vrt_camera *light_cam, const vrt_film *light_film,
+static int lightmap_enqueue(vrt_scene *s, int set, const vrt_camera *light_cam, const vrt_film *light_film,
                             unsigned int *hits, const std::function<int()> &overlap, hipEvent_t lm_done)
 {
         const int64_t nnodes = (int64_t)s->nodes.size();
@@ -1886,14 +1907,14 @@ static int lightmap_enqueue(vrt_scene *s, const vrt_camera *light_cam, const vrt
         if (ns > 0x7FFFFFFF)
                 return fail(VRT_E_INVALID, "light film too large (%lld samples)", (long long)ns);
         // one block: light map, cone-descent records, finiteness flag
-        if (!s->d_lm)
-                HIPCHK(hipMalloc(reinterpret_cast<void **>(&s->d_lm),
-                                 (size_t)nnodes * (sizeof(LMRec) + sizeof(float4)) + 256));
-        float4 *d_cc = reinterpret_cast<float4 *>(s->d_lm + nnodes);
-        uint32_t *d_bad = reinterpret_cast<uint32_t *>(d_cc + nnodes);
-        if (int rc = scratch_acquire(s, s->stream))  // a trace render may still read the light map
+        if (int rc = ensure_lm(s, set))
                 return rc;
-        HIPCHK(hipMemsetAsync(s->d_lm, 0, (size_t)nnodes * sizeof(LMRec), s->stream));
+        LMRec *d_lm = s->ts[set].lm;
+        float4 *d_cc = reinterpret_cast<float4 *>(d_lm + nnodes);
+        uint32_t *d_bad = reinterpret_cast<uint32_t *>(d_cc + nnodes);
+        if (int rc = ts_acquire(s, set, s->stream))  // a trace render may still read this set
+                return rc;
+        HIPCHK(hipMemsetAsync(d_lm, 0, (size_t)nnodes * sizeof(LMRec), s->stream));
         HIPCHK(hipMemsetAsync(d_bad, 0, 4, s->stream));
         // scratch (sized for every sample hitting): 64-bit keys and 32-bit
         // slots in + out, the per-hit (illum, normal) records and their copy
@@ -1945,19 +1966,19 @@ static int lightmap_enqueue(vrt_scene *s, const vrt_camera *light_cam, const vrt
         HIPCHK(hipStreamSynchronize(s->stream));
         if (nhit > 0)
                 HIPCHK(sort_pairs_u64(temp, &sort_bytes, k_in, k_out, v_in, v_out, nhit, kbits + lbits, s->stream));
-        HIPCHK(launch_lm_accum(nhit, k_out, v_out, kbits, samp, d_seg, d_nseg, max_seg, d_seg_end, s->d_lm,
+        HIPCHK(launch_lm_accum(nhit, k_out, v_out, kbits, samp, d_seg, d_nseg, max_seg, d_seg_end, d_lm,
                                s->stream));
         // cone_trace_init_filter: leaves, then internal levels bottom-up
-        HIPCHK(launch_lm_leaves(s->dev.nodes, nnodes, s->d_lm, s->stream));
+        HIPCHK(launch_lm_leaves(s->dev.nodes, nnodes, d_lm, s->stream));
         const int nlev = (int)s->level_begin.size() - 1;
         for (int l = nlev; l >= 1; --l)
-                HIPCHK(launch_lm_level(s->dev.nodes, s->level_begin[l - 1], s->level_begin[l], s->d_lm, s->stream));
-        HIPCHK(launch_lm_aux(s->dev.nodes, s->d_lm, nnodes, d_cc, d_bad, s->stream));
+                HIPCHK(launch_lm_level(s->dev.nodes, s->level_begin[l - 1], s->level_begin[l], d_lm, s->stream));
+        HIPCHK(launch_lm_aux(s->dev.nodes, d_lm, nnodes, d_cc, d_bad, s->stream));
         HIPCHK(hipEventRecord(s->ev1, s->stream));
         if (lm_done)
                 HIPCHK(hipEventRecord(lm_done, s->stream));
         s->timed = true;
-        s->lm_ready = true;
+        s->lm_cur = set;
         *hits = nhit;
         return VRT_OK;
 }
@@ -1974,9 +1995,11 @@ extern "C" int vrt_lightmap_build(vrt_scene *s, const vrt_camera *light_cam,
         std::lock_guard<std::mutex> lk(s->mu);
         HIPCHK(hipSetDevice(s->device));
         unsigned int nhit = 0;
-        if (int rc = lightmap_enqueue(s, light_cam, light_film, &nhit, {}, nullptr))
+        const int set = s->ts_next;
+        s->ts_next ^= 1;
+        if (int rc = lightmap_enqueue(s, set, light_cam, light_film, &nhit, {}, nullptr))
                 return rc;
-        if (int rc = scratch_release(s, s->stream))
+        if (int rc = ts_release(s, set, s->stream))
                 return rc;
         HIPCHK(hipStreamSynchronize(s->stream));
         if (hits)
@@ -1990,13 +2013,14 @@ extern "C" int vrt_lightmap_nodes(vrt_scene *s, uint64_t *key, float *coverage, 
                 return VRT_E_NODEVICE;
         if (!s || !key)
                 return fail(VRT_E_INVALID, "null argument");
-        if (!s->lm_ready)
+        if (s->lm_cur < 0)
                 return fail(VRT_E_INVALID, "no light map: call vrt_lightmap_build first");
         std::lock_guard<std::mutex> lk(s->mu);
         HIPCHK(hipSetDevice(s->device));
         const size_t n = s->nodes.size();
         std::vector<LMRec> lm(n);
-        HIPCHK(hipMemcpy(lm.data(), s->d_lm, n * sizeof(LMRec), hipMemcpyDeviceToHost));
+        HIPCHK(hipDeviceSynchronize());  // the set may be filled on another stream (trace frames)
+        HIPCHK(hipMemcpy(lm.data(), s->ts[s->lm_cur].lm, n * sizeof(LMRec), hipMemcpyDeviceToHost));
         for (size_t l = 0; l + 1 < s->level_begin.size(); ++l)
                 for (int64_t i = s->level_begin[l]; i < s->level_begin[l + 1]; ++i) {
                         key[i] = ((uint64_t)(l + 1) << 32) | s->node_vox[(size_t)i];
@@ -2032,26 +2056,25 @@ static bool trace_fused()
         return f;
 }
 
-static int trace_scratch(vrt_scene *s, const TraceParams &tp, TraceParams *out, hipStream_t st)
+static int trace_scratch(vrt_scene *s, int set, const TraceParams &tp, TraceParams *out)
 {
         *out = tp;
         if (trace_fused())
                 return VRT_OK;
+        TraceSet &t = s->ts[set];
         const size_t nslots = (size_t)tp.r.tiles_this_rank * 256;
         const size_t need = nslots * 64 + 512;  // the primary pass's 64-B records
-        if (s->trace_bytes < need) {
-                if (s->d_trace) {
+        if (t.rec_bytes < need) {
+                if (t.rec) {
                         HIPCHK(hipDeviceSynchronize());  // callers may have queued work on any stream
-                        (void)hipFree(s->d_trace);
-                        s->d_trace = nullptr;
-                        s->trace_bytes = 0;
+                        (void)hipFree(t.rec);
+                        t.rec = nullptr;
+                        t.rec_bytes = 0;
                 }
-                HIPCHK(hipMalloc(&s->d_trace, need));
-                s->trace_bytes = need;
+                HIPCHK(hipMalloc(&t.rec, need));
+                t.rec_bytes = need;
         }
-        (void)st;
-        char *base = static_cast<char *>(s->d_trace);
-        out->rec = reinterpret_cast<float4 *>(base);
+        out->rec = reinterpret_cast<float4 *>(t.rec);
         return VRT_OK;
 }
 
@@ -2107,15 +2130,15 @@ static void split_bounds(float maxdist, const float *up, float *bound)
         std::memcpy(last, bound, sizeof last);
 }
 
-static void fill_trace_params(vrt_scene *s, const vrt_camera *cam, const vrt_film *film, float min_voxel,
+static void fill_trace_params(vrt_scene *s, int set, const vrt_camera *cam, const vrt_film *film, float min_voxel,
                               int rank, int nranks, TraceParams *tp)
 {
         std::memset(tp, 0, sizeof *tp);
         fill_render_params(s, cam, film, rank, nranks, &tp->r);
         if (!(min_voxel > 0.f))
                 vrt_scene_min_voxel(s, 0, &min_voxel);
-        tp->lm = s->d_lm;
-        tp->cc = reinterpret_cast<const float4 *>(s->d_lm + s->nodes.size());
+        tp->lm = s->ts[set].lm;
+        tp->cc = reinterpret_cast<const float4 *>(s->ts[set].lm + s->nodes.size());
         tp->lm_bad = reinterpret_cast<const uint32_t *>(tp->cc + s->nodes.size());
         // float mindist = 1.414f * min_voxel_size; maxdist = length(root.aabb.size())
         tp->mindist = 1.414f * min_voxel;
@@ -2136,7 +2159,7 @@ extern "C" int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam, cons
                 return fail(VRT_E_INVALID, "null argument");
         if (int rc = film_ok(film))
                 return rc;
-        if (!s->lm_ready)
+        if (s->lm_cur < 0)
                 return fail(VRT_E_INVALID, "no light map: call vrt_lightmap_build first");
         if (nranks < 1 || rank < 0 || rank >= nranks)
                 return fail(VRT_E_INVALID, "rank %d of %d", rank, nranks);
@@ -2146,19 +2169,20 @@ extern "C" int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam, cons
                 return rc;
         std::lock_guard<std::mutex> lk(s->mu);
         HIPCHK(hipSetDevice(s->device));
+        const int set = s->lm_cur;  // the latest light map
         TraceParams tp0, tp;
-        fill_trace_params(s, cam, film, min_voxel, rank, nranks, &tp0);
+        fill_trace_params(s, set, cam, film, min_voxel, rank, nranks, &tp0);
         tp0.r.image_layout = image_layout;
         tp0.r.out = d_out;
         hipStream_t st = static_cast<hipStream_t>(stream);
-        if (int rc = trace_scratch(s, tp0, &tp, st))
+        if (int rc = trace_scratch(s, set, tp0, &tp))
                 return rc;
-        if (int rc = scratch_acquire(s, st))
+        if (int rc = ts_acquire(s, set, st))
                 return rc;
         HIPCHK(hipEventRecord(s->ev0, st));
         HIPCHK(launch_trace(tp, st));
         HIPCHK(hipEventRecord(s->ev1, st));
-        if (int rc = scratch_release(s, st))
+        if (int rc = ts_release(s, set, st))
                 return rc;
         s->timed = true;
         return VRT_OK;
@@ -2193,14 +2217,18 @@ extern "C" int vrt_trace_frame_device(vrt_scene *s, const vrt_camera *light_cam,
         hipStream_t st = static_cast<hipStream_t>(stream);
         if (!s->lm_ev)
                 HIPCHK(hipEventCreateWithFlags(&s->lm_ev, hipEventDisableTiming));
-        if (!s->d_lm)  // the trace parameters point into the light-map block
-                HIPCHK(hipMalloc(reinterpret_cast<void **>(&s->d_lm),
-                                 s->nodes.size() * (sizeof(LMRec) + sizeof(float4)) + 256));
+        // alternate sets: this frame's light pass waits only for the frame
+        // before last (the set's previous user), so it runs beside the
+        // previous frame's cone-traced shading
+        const int set = s->ts_next;
+        s->ts_next ^= 1;
+        if (int rc = ensure_lm(s, set))  // the trace parameters point into it
+                return rc;
         TraceParams tp0, tp;
-        fill_trace_params(s, cam, film, min_voxel, rank, nranks, &tp0);
+        fill_trace_params(s, set, cam, film, min_voxel, rank, nranks, &tp0);
         tp0.r.image_layout = image_layout;
         tp0.r.out = d_out;
-        if (int rc = trace_scratch(s, tp0, &tp, st))
+        if (int rc = trace_scratch(s, set, tp0, &tp))
                 return rc;
         if (!tp.rec)
                 return fail(VRT_E_INVALID, "vrt_trace_frame_device needs the split trace (VRT_TRACE_FUSED unset)");
@@ -2208,16 +2236,16 @@ extern "C" int vrt_trace_frame_device(vrt_scene *s, const vrt_camera *light_cam,
         auto overlap = [&]() -> int {
                 // the view's primary march beside the light pass (its records
                 // wait only for the previous frame's users of the scratch)
-                if (int rc = scratch_acquire(s, st))
+                if (int rc = ts_acquire(s, set, st))
                         return rc;
                 HIPCHK(launch_trace_prim(tp, st));
                 return VRT_OK;
         };
-        if (int rc = lightmap_enqueue(s, light_cam, light_film, &nhit, overlap, s->lm_ev))
+        if (int rc = lightmap_enqueue(s, set, light_cam, light_film, &nhit, overlap, s->lm_ev))
                 return rc;
         HIPCHK(hipStreamWaitEvent(st, s->lm_ev, 0));
         HIPCHK(launch_cones(tp, st));
-        if (int rc = scratch_release(s, st))
+        if (int rc = ts_release(s, set, st))
                 return rc;
         if (hits)
                 *hits = (int64_t)nhit;
@@ -2233,21 +2261,22 @@ extern "C" int vrt_render_trace(vrt_scene *s, const vrt_camera *cam, const vrt_f
                 return fail(VRT_E_INVALID, "null argument");
         if (int rc = film_ok(film))
                 return rc;
-        if (!s->lm_ready)
+        if (s->lm_cur < 0)
                 return fail(VRT_E_INVALID, "no light map: call vrt_lightmap_build first");
         if (int rc = trace_ok(s, min_voxel))
                 return rc;
         std::lock_guard<std::mutex> lk(s->mu);
         HIPCHK(hipSetDevice(s->device));
+        const int set = s->lm_cur;
         const size_t npix = (size_t)film->nx * film->ny, ns = npix * 4;
         DevBuf img, dh, dr;
         HIPCHK(hipMalloc(&img.p, npix * 12));
         HIPCHK(hipMemsetAsync(img.p, 0, npix * 12, s->stream));
         TraceParams tp0, tp;
-        fill_trace_params(s, cam, film, min_voxel, 0, 1, &tp0);
+        fill_trace_params(s, set, cam, film, min_voxel, 0, 1, &tp0);
         tp0.r.image_layout = 1;
         tp0.r.out = static_cast<float *>(img.p);
-        if (int rc = trace_scratch(s, tp0, &tp, s->stream))
+        if (int rc = trace_scratch(s, set, tp0, &tp))
                 return rc;
         if (s_hit) {
                 HIPCHK(hipMalloc(&dh.p, ns * 4));
@@ -2259,12 +2288,12 @@ extern "C" int vrt_render_trace(vrt_scene *s, const vrt_camera *cam, const vrt_f
                 HIPCHK(hipMemsetAsync(dr.p, 0, ns * 12, s->stream));
                 tp.r.so.rgb = static_cast<float *>(dr.p);
         }
-        if (int rc = scratch_acquire(s, s->stream))
+        if (int rc = ts_acquire(s, set, s->stream))
                 return rc;
         HIPCHK(hipEventRecord(s->ev0, s->stream));
         HIPCHK(launch_trace(tp, s->stream));
         HIPCHK(hipEventRecord(s->ev1, s->stream));
-        if (int rc = scratch_release(s, s->stream))
+        if (int rc = ts_release(s, set, s->stream))
                 return rc;
         s->timed = true;
         HIPCHK(hipStreamSynchronize(s->stream));
