@@ -396,9 +396,10 @@ def parse():
                         "unpacks; from 4 ranks on the deal gives it fewer tiles than the others)")
     p.add_argument("--rehearse-render-only", action="store_true",
                    help="with --rehearse-ranks: time the share's renders alone (no gather, no unpack)")
-    p.add_argument("--frames-in-flight-trace", type=int, default=2,
-                   help="frames in flight for --mode trace: the scene keeps two light-map / record sets, so a "
-                        "frame's light pass runs beside the previous frame's cone-traced shading")
+    p.add_argument("--frames-in-flight-trace", type=int, default=1,
+                   help="frames in flight for --mode trace (the scene keeps two light-map / record sets, so a "
+                        "frame's light pass can run beside the previous frame's cones; round 4: 1 / 2 in flight "
+                        "160.7 / 156.1 frames/s)")
     p.add_argument("--frames-in-flight-secondary", type=int, default=1,
                    help="frames in flight for --mode secondary (round 4, streaming resume round: 1 / 2 / 3 in "
                         "flight 17.81 / 17.85 / 18.08 ms per frame)")
