@@ -274,6 +274,10 @@ int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
  * every odd chunk of saved rays to its batch-pool launch (the path a chunk
  * with a degenerate ray takes). */
 #define VRT_TEST_STREAM_LEFTOVER 16
+/* VRT_TEST_LIGHT_TAIL makes the light pass hand every sample to its
+ * one-ray-per-wave tail launch (the path of samples whose walk passes the
+ * light pass's triangle-test budget). */
+#define VRT_TEST_LIGHT_TAIL 32
 #define VRT_TEST_VIRTUAL_RANKS_N(n) (VRT_TEST_VIRTUAL_RANKS | ((n) << 8))
 int vrt_set_test_flags(int flags);
 

@@ -513,6 +513,27 @@ def test_lightmap_and_trace_match_oracle(proxy_small, depth, light_n):
         assert np.array_equal(bits(rgb), bits(orgb))
 
 
+@pytest.mark.parametrize("depth,light_n", [(5, 96), (8, 128)])
+def test_lightmap_tail_walk_matches_oracle(proxy_small, depth, light_n):
+    """The light pass's tail launch (k_light_tail: one sample per wave, the
+    leaf records split over the lanes) for every sample (TEST_LIGHT_TAIL):
+    the light map is bit-exact vs the oracle, as with the budgeted walk."""
+    tree = vrt.VoxelOctree(proxy_small, depth)
+    osc = po.Scene(proxy_small, depth)
+    ohits = osc.lightmap(po.camera(*LIGHT), 1.0, 1.0, light_n, light_n, nthreads=8)
+    ok, ocov, oill = osc.lightmap_nodes()
+    vrt.set_test_flags(vrt.TEST_LIGHT_TAIL)
+    try:
+        hits = tree.lightmap(vrt.Camera(*LIGHT), vrt.Film(1, 1, light_n, light_n))
+    finally:
+        vrt.set_test_flags(0)
+    assert hits == ohits > 0
+    k, cov, ill = tree.lightmap_nodes()
+    assert np.array_equal(k, ok)
+    assert np.array_equal(bits(cov), bits(ocov))
+    assert np.array_equal(bits(ill), bits(oill))
+
+
 def test_trace_device_tiles_reassemble(proxy_small):
     import torch
     tree = vrt.VoxelOctree(proxy_small, 6)

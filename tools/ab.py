@@ -37,9 +37,9 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--poses", type=int, default=16)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--width", type=int, default=None, help="default 1920 (1024 for --mode trace)")
+    ap.add_argument("--height", type=int, default=None, help="default 1080 (1024 for --mode trace)")
+    ap.add_argument("--depth", type=int, default=None, help="default 8 (6 for --mode trace, as bench.py)")
     ap.add_argument("--detail", type=float, default=1.0)
     ap.add_argument("--mode", default="primary", choices=["primary", "secondary", "trace"])
     ap.add_argument("--light-n", type=int, default=2048, help="--mode trace: light film side (VRT/main.cc:79)")
@@ -50,6 +50,10 @@ def main():
                          "per pose the slowest rank counts, as in an N-GPU step), images re-assembled with each "
                          "variant's own vrt_unpack_tiles_device for the parity check")
     a = ap.parse_args()
+    tr = a.mode == "trace"
+    a.width = a.width or (1024 if tr else 1920)
+    a.height = a.height or (1024 if tr else 1080)
+    a.depth = a.depth or (6 if tr else 8)
     sd = vrt.SceneData.proxy(a.detail, 1)
     film = _ffi.Film(1.0, 1.0, a.width, a.height)
     libs = [load(p) for p in a.libs]
@@ -169,6 +173,7 @@ def trace_ab(a, libs, scenes, film):
     imgs = [torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev) for _ in libs]
     times = {p: [] for p in a.libs}
     ltimes = {p: [] for p in a.libs}
+    ftimes = {p: [] for p in a.libs}
     ref = None
     for r in range(a.rounds + 1):
         for vi, (L, h, p) in enumerate(zip(libs, scenes, a.libs)):
@@ -198,13 +203,29 @@ def trace_ab(a, libs, scenes, film):
                     raise SystemExit(f"variant {p} differs from baseline {a.libs[0]}")
             else:
                 times[p].append(sum(s_.elapsed_time(e_) for s_, e_ in evs) / len(evs))
+            # the whole frame in one call (vrt_trace_frame_device), 4 frames
+            if hasattr(L, "vrt_trace_frame_device"):
+                t0 = time.perf_counter()
+                for _ in range(4):
+                    rc = L.vrt_trace_frame_device(h, C.byref(light), C.byref(lfilm), C.byref(view), C.byref(film),
+                                                  0.0, 0, 1, 1, C.c_void_p(imgs[vi].data_ptr()),
+                                                  C.c_void_p(st.cuda_stream), C.byref(hits))
+                    assert rc == 0, L.vrt_last_error()
+                torch.cuda.synchronize()
+                if r > 0:
+                    ftimes[p].append((time.perf_counter() - t0) * 1e3 / 4)
     base = np.median(times[a.libs[0]])
+    fbase = np.median(ftimes[a.libs[0]]) if ftimes[a.libs[0]] else None
     lbase = np.median(ltimes[a.libs[0]])
     print(json.dumps({os.path.basename(p): {"median_ms": round(float(np.median(t)), 4),
                                             "min_ms": round(float(np.min(t)), 4),
                                             "speedup": round(float(base / np.median(t)), 3),
                                             "lightmap_wall_ms": round(float(np.median(ltimes[p])), 4),
-                                            "lightmap_speedup": round(float(lbase / np.median(ltimes[p])), 3)}
+                                            "lightmap_speedup": round(float(lbase / np.median(ltimes[p])), 3),
+                                            "frame_wall_ms": (round(float(np.median(ftimes[p])), 4)
+                                                              if ftimes[p] else None),
+                                            "frame_speedup": (round(float(fbase / np.median(ftimes[p])), 3)
+                                                              if ftimes[p] and fbase else None)}
                       for p, t in times.items()}, indent=1))
 
 

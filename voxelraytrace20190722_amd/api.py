@@ -710,6 +710,7 @@ TEST_FAIL_LAUNCH = 2  # include/vrt.h VRT_TEST_FAIL_LAUNCH
 TEST_SPILL_ALL = 4  # include/vrt.h VRT_TEST_SPILL_ALL
 TEST_VIRTUAL_RANKS = 8  # include/vrt.h VRT_TEST_VIRTUAL_RANKS (count << 8)
 TEST_STREAM_LEFTOVER = 16  # include/vrt.h VRT_TEST_STREAM_LEFTOVER
+TEST_LIGHT_TAIL = 32  # include/vrt.h VRT_TEST_LIGHT_TAIL
 
 
 def set_test_flags(flags):

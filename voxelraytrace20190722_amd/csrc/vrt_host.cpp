@@ -1955,6 +1955,8 @@ static int lightmap_enqueue(vrt_scene *s, int set, const vrt_camera *light_cam, 
         lp.keys = k_in;
         lp.vals = v_in;
         lp.samp = samp;
+        lp.tail_n = reinterpret_cast<unsigned int *>(tail + 128);
+        lp.tail = v_out;  // free until the sort
         HIPCHK(hipEventRecord(s->ev0, s->stream));
         HIPCHK(launch_light(lp, s->stream));
         if (overlap)
@@ -1964,6 +1966,27 @@ static int lightmap_enqueue(vrt_scene *s, int set, const vrt_camera *light_cam, 
         unsigned int nhit = 0;
         HIPCHK(hipMemcpyAsync(&nhit, d_count, sizeof nhit, hipMemcpyDeviceToHost, s->stream));
         HIPCHK(hipStreamSynchronize(s->stream));
+#ifdef VRT_LIGHT_DIAG
+        {
+                static int ndump = 0;
+                const size_t nw = (size_t)std::min<int64_t>(ns / 64, 1 << 20);
+                std::vector<uint32_t> d(nw * 8);
+                HIPCHK(light_diag_copy(d.data(), d.size() * 4));
+                char name[64];
+                std::snprintf(name, sizeof name, "gpurun_out/light_diag_%d.bin", ndump++);
+                if (FILE *f = std::fopen(name, "wb")) {
+                        std::fwrite(d.data(), 4, d.size(), f);
+                        std::fclose(f);
+                }
+        }
+#endif
+#ifdef VRT_LIGHT_TAIL_REPORT
+        {
+                unsigned int ntail = 0;
+                HIPCHK(hipMemcpy(&ntail, lp.tail_n, sizeof ntail, hipMemcpyDeviceToHost));
+                std::fprintf(stderr, "light pass: %u of %lld samples deferred, %u hits\n", ntail, (long long)ns, nhit);
+        }
+#endif
         if (nhit > 0)
                 HIPCHK(sort_pairs_u64(temp, &sort_bytes, k_in, k_out, v_in, v_out, nhit, kbits + lbits, s->stream));
         HIPCHK(launch_lm_accum(nhit, k_out, v_out, kbits, samp, d_seg, d_nseg, max_seg, d_seg_end, d_lm,

@@ -446,6 +446,8 @@ struct LightParams {
         uint64_t *keys;
         uint32_t *vals;
         float *samp;
+        unsigned int *tail_n;  // deferred samples (k_light_tail): count, then work unit << 6 | lane
+        uint32_t *tail;
 };
 
 // Cone-tracing render (trace(), VRT/main.cc:10-30 + cone_trace,
@@ -527,6 +529,7 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,
 // the compaction settings of this build (VRT_SEC_SPILL*), cap left 0
 SpillQueues spill_defaults();
 hipError_t launch_light(const LightParams &p, hipStream_t st);
+hipError_t light_diag_copy(void *host, size_t bytes);  // VRT_LIGHT_DIAG builds
 // samp: n x 6 floats followed by room for their sorted copy (n x 6);
 // seg_start: max_seg entries (>= non-empty leaves), nseg zeroed; seg_end:
 // one entry per node (each hit leaf's run end is written)

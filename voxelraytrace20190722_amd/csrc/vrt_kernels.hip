@@ -159,14 +159,26 @@ __device__ __forceinline__ void wave_lds_sync()
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-#if VRT_PHASE_STAMPS
-__device__ unsigned long long g_phase[16];
+// Diagnostic build only (VRT_LIGHT_DIAG=1): per light-pass wave, its walk's
+// cycles and per-lane node visits / leaf phases / triangle tests (maximum and
+// sum over the lanes), dumped by the host after each light pass.
+#ifndef VRT_LIGHT_DIAG
+#define VRT_LIGHT_DIAG 0
+#endif
+#if VRT_LIGHT_DIAG
+constexpr int kLightDiagWaves = 1 << 20;
+__device__ uint32_t g_light_diag[kLightDiagWaves * 8];
+#endif
+#if VRT_PHASE_STAMPS || VRT_LIGHT_DIAG
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
 {
         for (int o = 32; o > 0; o >>= 1)
                 v += (uint32_t)__shfl_xor((int)v, o, 64);
         return v;
 }
+#endif
+#if VRT_PHASE_STAMPS
+__device__ unsigned long long g_phase[16];
 #endif
 
 // ---------------------------------------------------------------------------
@@ -550,6 +562,7 @@ struct MarchResult {
         float u, v;     // clamped barycentrics of the best triangle
         f3 hp;          // ISect::hit
         uint32_t A, L, T;  // reference-equivalent counters (instrumented)
+        bool deferred;  // the walk stopped at its record budget (ray_march kBudget)
 };
 
 // ray_march_isect's std::min_element over the records (VRT/voxel_octree.cc:
@@ -747,10 +760,81 @@ __device__ __forceinline__ bool leaf_isect_uni(const RefRec64 *__restrict__ recs
         return any;
 }
 
-template <bool kCount, bool kUni, bool kR64>
+// minimum / OR over each aligned group of kG lanes (every lane of the group
+// active)
+template <int kG>
+__device__ __forceinline__ uint64_t group_min_u64(uint64_t v)
+{
+#pragma unroll
+        for (int o = kG / 2; o > 0; o >>= 1) {
+                const uint64_t w = (uint64_t)__shfl_xor((long long)v, o, 64);
+                v = w < v ? w : v;
+        }
+        return v;
+}
+template <int kG>
+__device__ __forceinline__ uint32_t group_or_u32(uint32_t v)
+{
+#pragma unroll
+        for (int o = kG / 2; o > 0; o >>= 1)
+                v |= (uint32_t)__shfl_xor((int)v, o, 64);
+        return v;
+}
+
+// One ray per aligned group of kG lanes (every lane of a group holds the
+// same ray and walks the same leaf): the leaf's records are split over the
+// group (lane l tests records l % kG, + kG, ...) and the winner is
+// ray_march_isect's first minimum over the whole leaf.  A lane's own first
+// minimum is exact for its records unless its first hit had a NaN depth
+// (which std::min_element would then keep); a NaN kept by any lane of the
+// group sends the leaf through the serial loop (the group's lanes alike).
+// Otherwise the leaf's winner is the least (depth, record) pair -- depth >=
+// +0, so its float bits order as integers -- and every lane of the group
+// re-tests that one record to take its (tri, u, v, hit) exactly as the
+// serial loop would.
+template <int kG, bool kR64>
+__device__ __forceinline__ bool leaf_isect_grp(const void *__restrict__ refs, uint32_t first, uint32_t n,
+                                               const RayK &r, MarchResult &m)
+{
+        bool any = false;
+        float best = 0.f, best_t = 0.f;
+        uint32_t kb = 0;
+        for (uint32_t k = lane_id() & (kG - 1); k < n; k += kG) {
+                const float4 *q = kR64 ? reinterpret_cast<const float4 *>(static_cast<const RefRec64 *>(refs) + first + k)
+                                       : reinterpret_cast<const float4 *>(static_cast<const RefRec48 *>(refs) + first + k);
+                const double2 *qd = reinterpret_cast<const double2 *>(q);
+                const float4 q0 = q[0];
+                float4 q1 = q0, q2 = q0;
+                double2 qd1 = {}, qd2 = {}, qd3 = {};
+                if (kR64) {
+                        qd1 = qd[1];
+                        qd2 = qd[2];
+                        qd3 = qd[3];
+                } else {
+                        q1 = q[1];
+                        q2 = q[2];
+                }
+                if (mt_record<kR64>(q0, q1, q2, qd1, qd2, qd3, r, any, best, best_t, m))
+                        kb = k;
+        }
+        if (group_or_u32<kG>(any && isnan(best) ? 1u : 0u))
+                return leaf_isect_v2<false, kR64>(refs, first, n, r, m);
+        const uint64_t key = any ? ((uint64_t)__float_as_uint(best) << 32 | kb) : ~0ull;
+        const uint64_t win = group_min_u64<kG>(key);
+        if (win == ~0ull)
+                return false;
+        return leaf_isect_v2<false, kR64>(refs, first + (uint32_t)win, 1, r, m);
+}
+
+// kUni: 0 each lane its own leaf, 1 the same leaf may be shared (scalar
+// loads when every lane tests it), >= 2 (a power of two) one ray per group
+// of kUni lanes (leaf_isect_grp)
+template <bool kCount, int kUni, bool kR64>
 __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, uint32_t n,
                                            const RayK &r, MarchResult &m)
 {
+        if (kUni >= 2)
+                return leaf_isect_grp<(kUni >= 2 ? kUni : 2), kR64>(sc.refs, first, n, r, m);
 #ifndef VRT_LEAF_UNIFORM
 #define VRT_LEAF_UNIFORM 1
 #endif
@@ -797,7 +881,9 @@ __device__ __forceinline__ bool leaf_box_ok(const DevScene &sc, const RayK &r)
 // reads DevScene::mnodes and skips a leaf whose triangles' box the ray's
 // line misses (no triangle of it can pass; the leaf is left as the reference
 // leaves it, with no record).
-template <bool kCount, bool kFast, int kS, int kStd, bool kUni, bool kR64, int kNS = 0>
+// kBudget > 0: the walk gives up (m.deferred) before a leaf that would take
+// its triangle tests past kBudget; a caller re-walks such a ray elsewhere.
+template <bool kCount, bool kFast, int kS, int kStd, int kUni, bool kR64, int kNS = 0, int kBudget = 0>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint2 *stk,
                                           uint32_t *stk_aux,
@@ -805,9 +891,11 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           MarchResult &m)
 {
         m.hit = false;
+        m.deferred = false;
         m.A = 1;
         m.L = 0;
         m.T = 0;
+        uint32_t used = 0;  // triangle tests so far (kBudget)
         float bmin[3], bmax[3];
         uint32_t a, b;
         constexpr bool kLB = kFast && kStd == 2 && !kCount;
@@ -844,6 +932,9 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         uint32_t d_it = 0, d_lp = 0, d_tri = 0, d_lpmax = 0, d_lpsum = 0, d_phmax = 0;
         unsigned long long d_tin = 0, d_tleaf = 0;
 #endif
+#if VRT_LIGHT_DIAG
+        uint32_t dg_it = 0, dg_lp = 0, dg_tri = 0;
+#endif
         for (;;) {
                 bool leaf = false;
                 uint32_t node = 0, nref = 0;
@@ -856,6 +947,9 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 for (;;) {
 #if VRT_PHASE_STAMPS
                         ++d_it;
+#endif
+#if VRT_LIGHT_DIAG
+                        ++dg_it;
 #endif
                         if (cnt == 0) {
                                 if (sp == 0)
@@ -933,9 +1027,20 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
 #endif
                 if (!leaf)
                         break;
+                if (kBudget) {
+                        used += nref;
+                        if (used > (uint32_t)kBudget) {
+                                m.deferred = true;
+                                break;
+                        }
+                }
 #if VRT_PHASE_STAMPS
                 ++d_lp;
                 d_tri += nref;
+#endif
+#if VRT_LIGHT_DIAG
+                ++dg_lp;
+                dg_tri += nref;
 #endif
                 const bool lh = leaf_isect<kCount, kUni, kR64>(sc, b, nref, r, m);
 #if VRT_PHASE_STAMPS
@@ -1027,6 +1132,11 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 }
         }
 #endif
+#if VRT_LIGHT_DIAG && VRT_WHILE_WHILE
+        m.A = dg_it;
+        m.L = dg_lp;
+        m.T = dg_tri;
+#endif
         if (kCount) {
                 // 1 root test + 8 per expanded node, minus the children the
                 // reference never popped on the path it stopped on.
@@ -1076,7 +1186,7 @@ __device__ __forceinline__ bool fin_ok(const RayK &r)
                fabsf(r.dinv.z) <= 0x1p64f;
 }
 
-template <bool kCount, int kS, bool kUni, bool kR64, int kNS = 0>
+template <bool kCount, int kS, int kUni, bool kR64, int kNS = 0, int kBudget = 0>
 __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const RayK &r,
                                                    uint2 *sb, uint32_t *sa, uint32_t *pr,
                                                    MarchResult &m)
@@ -1086,13 +1196,13 @@ __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const Ray
 #endif
         if (__all(sc.fast_ok && fast_ok(r))) {
                 if (VRT_FIN && !kCount && __all(fin_ok(r)))
-                        ray_march<kCount, true, kS, 2, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, 2, kUni, kR64, kNS, kBudget>(sc, r, sb, sa, pr, m);
                 else if (!VRT_FIN && VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
-                        ray_march<kCount, true, kS, 1, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, 1, kUni, kR64, kNS, kBudget>(sc, r, sb, sa, pr, m);
                 else
-                        ray_march<kCount, true, kS, 0, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, 0, kUni, kR64, kNS, kBudget>(sc, r, sb, sa, pr, m);
         } else
-                ray_march<kCount, false, kS, 0, kUni, kR64, kNS>(sc, r, sb, sa, pr, m);
+                ray_march<kCount, false, kS, 0, kUni, kR64, kNS, kBudget>(sc, r, sb, sa, pr, m);
 }
 
 // True when ray_march's fast instantiation for camera rays is exact for
@@ -3476,10 +3586,35 @@ __device__ __forceinline__ int xcd_place(int b, int nb)
         return (b & 7) * (nb >> 3) + (b >> 3);
 }
 
+// Block b -> work unit with the units dealt to the XCDs in chunks of kC
+// consecutive units (chunk j to XCD j % 8), so a dense region of the film
+// (a run of heavy units) is shared by all eight XCDs instead of landing on
+// one or two of them, as xcd_place's contiguous eighths put it.  kC = 0:
+// xcd_place.  Units past the last whole chunk round keep xcd_place's order.
+template <int kC>
+__device__ __forceinline__ int chunk_place(int b, int nb)
+{
+        if (kC == 0)
+                return xcd_place(b, nb);
+        const int x = b & 7, i = b >> 3, per = nb >> 3, full = per / kC * kC;
+        if (i >= full)
+                return 8 * full + x * (per - full) + (i - full);
+        return ((i / kC) * 8 + x) * kC + i % kC;
+}
+#ifndef VRT_LIGHT_CHUNK
+#define VRT_LIGHT_CHUNK 16
+#endif
+#ifndef VRT_PRIM_CHUNK
+#define VRT_PRIM_CHUNK 0
+#endif
+#ifndef VRT_CONES_CHUNK
+#define VRT_CONES_CHUNK 0
+#endif
+
 // 8x8-pixel tile of work unit u and this lane's pixel / sample.  Returns
 // false for padding units.
-__device__ __forceinline__ bool tile_lane(const RenderParams &p, int u, int &k, int &px, int &py,
-                                          int &s, int &lx, int &ly)
+__device__ __forceinline__ bool tile_lane_at(const RenderParams &p, int u, int tid, int &k, int &px, int &py,
+                                             int &s, int &lx, int &ly)
 {
         constexpr int kQ = 4 / VRT_RENDER_WAVES;  // work units per tile
         if (u >= p.tiles_this_rank * kQ)
@@ -3487,7 +3622,7 @@ __device__ __forceinline__ bool tile_lane(const RenderParams &p, int u, int &k, 
         k = u / kQ;
         int tx, ty;
         deal_tile(tile_deal(p.ntx, p.nty, p.nranks), p.rank, k, tx, ty);
-        const int tid = threadIdx.x, wave = (u % kQ) * VRT_RENDER_WAVES + (tid >> 6), lane = tid & 63;
+        const int wave = (u % kQ) * VRT_RENDER_WAVES + (tid >> 6), lane = tid & 63;
         s = lane & 3;
         const int pix = lane >> 2;
         lx = (wave & 1) * 4 + (pix & 3);
@@ -3496,23 +3631,37 @@ __device__ __forceinline__ bool tile_lane(const RenderParams &p, int u, int &k, 
         py = ty * 8 + ly;
         return true;
 }
-
-template <bool kR64>
-__device__ __forceinline__ void light_unit(const LightParams &p, uint2 *stk, int u)
+__device__ __forceinline__ bool tile_lane(const RenderParams &p, int u, int &k, int &px, int &py,
+                                          int &s, int &lx, int &ly)
 {
-        const int tid = threadIdx.x;
-        int k, px, py, s, lx, ly;
-        if (!tile_lane(p.r, u, k, px, py, s, lx, ly))
-                return;
+        return tile_lane_at(p, u, (int)threadIdx.x, k, px, py, s, lx, ly);
+}
+
+// Light-pass walks are budgeted: a sample whose walk would pass
+// VRT_LIGHT_BUDGET triangle tests is handed (its work unit and lane) to
+// k_light_tail, which re-walks it from the root with a group of lanes on
+// that one ray (leaf_isect_grp).  The light pass's longest waves are whole
+// waves of samples landing in the large leaves under dense geometry (up to
+// ~2000 serial triangle tests per lane).
+#ifndef VRT_LIGHT_BUDGET
+#define VRT_LIGHT_BUDGET 256
+#endif
+#ifndef VRT_LIGHT_TAIL_GRID
+#define VRT_LIGHT_TAIL_GRID 8192
+#endif
+
+__device__ __forceinline__ RayK light_ray(const LightParams &p, int px, int py, int s)
+{
         const CamParams &c = p.r.cam;
         const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
                                  sample_x(s), sample_y(s));
-        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
-                                 dn, c.tmin, c.tmax);
-        MarchResult m;
-        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
-        if (!m.hit)
-                return;
+        return make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]), dn, c.tmin, c.tmax);
+}
+
+// one light-map sample record for a hit (m.hit) of sample (px, py, s)
+__device__ __forceinline__ void light_record(const LightParams &p, const RayK &r, const MarchResult &m, int px,
+                                             int py, int s)
+{
         // canonical order: render_mt task t = tx*8 + ty (VRT/camera.h:50-56)
         const int tx = px / p.ptx, ty = py / p.pty;
         const int64_t task = (int64_t)tx * 8 + ty;
@@ -3528,10 +3677,81 @@ __device__ __forceinline__ void light_unit(const LightParams &p, uint2 *stk, int
 }
 
 template <bool kR64>
+__device__ __forceinline__ void light_unit(const LightParams &p, uint2 *stk, int u)
+{
+        const int tid = threadIdx.x;
+        int k, px, py, s, lx, ly;
+        if (!tile_lane(p.r, u, k, px, py, s, lx, ly))
+                return;
+        const RayK r = light_ray(p, px, py, s);
+        MarchResult m;
+#if VRT_LIGHT_DIAG
+        const uint64_t dg_t0 = __builtin_amdgcn_s_memtime();
+        m.A = m.L = m.T = 0;
+#endif
+        if (p.r.test_flags & VRT_TEST_LIGHT_TAIL)
+                m.deferred = true;  // test hook: every sample to k_light_tail
+        else
+                ray_march_dispatch<false, kRenderBlock, 1, kR64, 0, VRT_LIGHT_BUDGET>(p.r.sc, r, stk + tid, nullptr,
+                                                                                     nullptr, m);
+#if VRT_LIGHT_DIAG
+        {
+                const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memtime() - dg_t0);
+                const uint32_t v[8] = { dt, wave_max_u32(m.A), wave_sum_u32(m.A), wave_max_u32(m.L),
+                                        wave_sum_u32(m.L), wave_max_u32(m.T), wave_sum_u32(m.T),
+                                        wave_sum_u32(m.hit ? 1u : 0u) };
+                if (lane_id() < 8 && u < kLightDiagWaves) {
+                        uint32_t x = v[0];
+#pragma unroll
+                        for (int q = 1; q < 8; ++q)
+                                x = lane_id() == (uint32_t)q ? v[q] : x;
+                        g_light_diag[(size_t)u * 8 + lane_id()] = x;
+                }
+        }
+#endif
+        if (m.deferred) {
+                const uint32_t j = atomicAdd(p.tail_n, 1u);
+                p.tail[j] = (uint32_t)u << 6 | (uint32_t)tid;
+                return;
+        }
+        if (m.hit)
+                light_record(p, r, m, px, py, s);
+}
+
+template <bool kR64>
 __global__ __launch_bounds__(kRenderBlock) void k_light(LightParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
-        light_unit<kR64>(p, stk, xcd_place(blockIdx.x, gridDim.x));
+        light_unit<kR64>(p, stk, chunk_place<VRT_LIGHT_CHUNK>(blockIdx.x, gridDim.x));
+}
+
+// The light pass's deferred samples, one per group of VRT_LIGHT_TAIL_G
+// lanes (see VRT_LIGHT_BUDGET): a group walks its sample's ray from the
+// root, its lanes alike, with the leaves' records split over them.  Same
+// result as the budgeted walk would have reached.
+#ifndef VRT_LIGHT_TAIL_G
+#define VRT_LIGHT_TAIL_G 8
+#endif
+template <bool kR64>
+__global__ __launch_bounds__(64) void k_light_tail(LightParams p)
+{
+        constexpr int kG = VRT_LIGHT_TAIL_G, kR = 64 / kG;  // lanes per sample, samples per wave
+        __shared__ uint2 stk[kStack * 64];
+        const uint32_t n = *p.tail_n;
+        const uint32_t gl = threadIdx.x & (kG - 1);
+        for (uint32_t i0 = blockIdx.x * kR; i0 < n; i0 += gridDim.x * kR) {
+                const uint32_t i = i0 + threadIdx.x / kG;
+                if (i < n) {  // whole groups
+                        const uint32_t slot = p.tail[i];
+                        int k, px, py, s, lx, ly;
+                        tile_lane_at(p.r, (int)(slot >> 6), (int)(slot & 63), k, px, py, s, lx, ly);
+                        const RayK r = light_ray(p, px, py, s);
+                        MarchResult m;
+                        ray_march_dispatch<false, 64, kG, kR64>(p.r.sc, r, stk + threadIdx.x, nullptr, nullptr, m);
+                        if (m.hit && gl == 0)
+                                light_record(p, r, m, px, py, s);
+                }
+        }
 }
 
 // Permute the per-sample records into the sorted (leaf, canonical) order so
@@ -4045,7 +4265,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
         const int tid = threadIdx.x, lane = tid & 63;
-        const int u = xcd_place(blockIdx.x, gridDim.x);
+        const int u = chunk_place<VRT_CONES_CHUNK>(blockIdx.x, gridDim.x);
         int k, px, py, s, lx, ly;
         if (!tile_lane(p.r, u, k, px, py, s, lx, ly))
                 return;
@@ -4137,7 +4357,7 @@ template <bool kR64>
 __global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
-        trace_prim_unit<kR64>(p, stk, xcd_place(blockIdx.x, gridDim.x));
+        trace_prim_unit<kR64>(p, stk, chunk_place<VRT_PRIM_CHUNK>(blockIdx.x, gridDim.x));
 }
 
 // Cones + film: one wave per work unit of the primary pass (its 64 sample
@@ -4222,12 +4442,27 @@ __global__ __launch_bounds__(64, VRT_CONES_WAVES_PER_EU) void k_cones_film(Trace
         }
 }
 
+// VRT_LIGHT_DIAG builds: the per-wave records of the last light pass
+hipError_t light_diag_copy(void *host, size_t bytes)
+{
+#if VRT_LIGHT_DIAG
+        return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_light_diag), bytes);
+#else
+        (void)host;
+        (void)bytes;
+        return hipErrorNotSupported;
+#endif
+}
+
 hipError_t launch_light(const LightParams &p, hipStream_t st)
 {
         if (p.r.tiles_this_rank <= 0)
                 return hipSuccess;
         const int grid = trace_vblocks(p.r.tiles_this_rank);
         hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_light<true> : k_light<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
+        if (VRT_LIGHT_BUDGET > 0 || (p.r.test_flags & VRT_TEST_LIGHT_TAIL))
+                hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_light_tail<true> : k_light_tail<false>,
+                                   dim3(VRT_LIGHT_TAIL_GRID), dim3(64), 0, st, p);
         return hipGetLastError();
 }
 
