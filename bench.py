@@ -938,7 +938,10 @@ def main():
                 # the frame's kernels (trace: light pass, light map, render;
                 # config 5: primary hits, the secondary walk and its resume
                 # rounds), each against its own rocprof time; the line's
-                # roofline = the one with the most time per frame
+                # roofline = the one with the most VALU work per frame (kernel
+                # time would pick the light pass of a trace frame, stretched
+                # by the primary march it runs beside, not on the frame's
+                # critical path)
                 trace_kernels = {}
                 for k in cand:
                     if k in ks:
@@ -955,8 +958,8 @@ def main():
                                             "rocprof_avg_ms": round(avg, 4), "rocprof_calls": calls,
                                             "note": "rocprofv3 kernel trace of this command (one frame in flight)"}
                         trace_kernels[k] = r_
-                dom = max(trace_kernels, key=lambda k: trace_kernels[k]["time_basis"]["rocprof_ms_per_frame"]) \
-                    if trace_kernels else None
+                dom = max(trace_kernels, key=lambda k: trace_kernels[k]["valu_instr_per_launch"]
+                          * trace_kernels[k]["time_basis"]["dispatches_per_frame"]) if trace_kernels else None
                 roof = dict(trace_kernels[dom]) if dom else None
                 if roof and trace:
                     roof["traffic_over_output"] = None  # the frame writes only the 1024^2 image

@@ -177,6 +177,18 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
         return v;
 }
 #endif
+// Diagnostic build only (VRT_UNIT_DIAG=1): per unit of the persistent
+// render: its start / end time (low 32 bits of s_memrealtime, 100 MHz: the
+// one clock all XCDs share), the wave that ran it and its slice, dumped by
+// the host after each launch (tools/unit_tail.py reads them).
+#ifndef VRT_UNIT_DIAG
+#define VRT_UNIT_DIAG 0
+#endif
+#if VRT_UNIT_DIAG
+constexpr int kUnitDiagMax = 1 << 20;
+__device__ uint32_t g_unit_diag[kUnitDiagMax * 4];
+__device__ uint32_t g_unit_walk[kUnitDiagMax * 4];  // with VRT_LIGHT_DIAG: wave max / sum of node visits, triangle tests
+#endif
 #if VRT_PHASE_STAMPS
 __device__ unsigned long long g_phase[16];
 #endif
@@ -932,9 +944,9 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         uint32_t d_it = 0, d_lp = 0, d_tri = 0, d_lpmax = 0, d_lpsum = 0, d_phmax = 0;
         unsigned long long d_tin = 0, d_tleaf = 0;
 #endif
-#if VRT_LIGHT_DIAG
+        // VRT_LIGHT_DIAG builds: node visits, leaf phases and triangle tests
+        // of this lane's walk, into m.A / m.L / m.T
         uint32_t dg_it = 0, dg_lp = 0, dg_tri = 0;
-#endif
         for (;;) {
                 bool leaf = false;
                 uint32_t node = 0, nref = 0;
@@ -948,9 +960,8 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
 #if VRT_PHASE_STAMPS
                         ++d_it;
 #endif
-#if VRT_LIGHT_DIAG
-                        ++dg_it;
-#endif
+                        if (VRT_LIGHT_DIAG)
+                                ++dg_it;
                         if (cnt == 0) {
                                 if (sp == 0)
                                         break;
@@ -1038,10 +1049,10 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 ++d_lp;
                 d_tri += nref;
 #endif
-#if VRT_LIGHT_DIAG
-                ++dg_lp;
-                dg_tri += nref;
-#endif
+                if (VRT_LIGHT_DIAG) {
+                        ++dg_lp;
+                        dg_tri += nref;
+                }
                 const bool lh = leaf_isect<kCount, kUni, kR64>(sc, b, nref, r, m);
 #if VRT_PHASE_STAMPS
                 d_tleaf += __builtin_amdgcn_s_memtime() - d_t1;
@@ -1131,11 +1142,11 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         break;
                 }
         }
-#endif
-#if VRT_LIGHT_DIAG && VRT_WHILE_WHILE
-        m.A = dg_it;
-        m.L = dg_lp;
-        m.T = dg_tri;
+        if (VRT_LIGHT_DIAG) {
+                m.A = dg_it;
+                m.L = dg_lp;
+                m.T = dg_tri;
+        }
 #endif
         if (kCount) {
                 // 1 root test + 8 per expanded node, minus the children the
@@ -1907,6 +1918,14 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         } else {
                 ray_march_dispatch<kCount, kS, true, kR64, kNS>(p.sc, r, stk, stk_aux, path_rem, m);
         }
+#if VRT_UNIT_DIAG && VRT_LIGHT_DIAG
+        if (kFastOnly) {
+                const uint32_t v[4] = { wave_max_u32(m.A), wave_sum_u32(m.A), wave_max_u32(m.T), wave_sum_u32(m.T) };
+                const int ku = k * 4 + wave;
+                if (lane < 4 && ku < kUnitDiagMax)
+                        g_unit_walk[(size_t)ku * 4 + lane] = lane == 0 ? v[0] : lane == 1 ? v[1] : lane == 2 ? v[2] : v[3];
+        }
+#endif
         // persistent kernels: the pixel (and with VRT_REDIR the direction)
         // are made again -- the same operations, so the same bits -- rather
         // than held live across the march
@@ -2073,8 +2092,21 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
 #if VRT_PHASE_STAMPS
                         const unsigned long long d_u0 = __builtin_amdgcn_s_memtime();
 #endif
+#if VRT_UNIT_DIAG
+                        const uint32_t dg_u0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
                         const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kNS>(
                                 p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr);
+#if VRT_UNIT_DIAG
+                        {
+                                const uint32_t dg_u1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                                const uint32_t v[4] = { dg_u0, dg_u1, (uint32_t)(blockIdx.x * 4 + (tid >> 6)),
+                                                        (uint32_t)x };
+                                if (lane < 4 && kq < kUnitDiagMax)
+                                        g_unit_diag[(size_t)kq * 4 + lane] =
+                                                lane == 0 ? v[0] : lane == 1 ? v[1] : lane == 2 ? v[2] : v[3];
+                        }
+#endif
 #if VRT_PHASE_STAMPS
                         if (lane == 0)
                                 atomicAdd(&g_phase[10], __builtin_amdgcn_s_memtime() - d_u0);
@@ -3433,6 +3465,31 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                         hipLaunchKernelGGL(k_render_p<true>, dim3(g), dim3(kPersistBlock), 0, st, p);
                         if (hipError_t e = hipGetLastError())
                                 return e;
+#if VRT_UNIT_DIAG
+                        {
+                                static int ndump = 0;
+                                const size_t nu = std::min<size_t>((size_t)p.tiles_this_rank * 4, kUnitDiagMax);
+                                std::vector<uint32_t> d(nu * 4);
+                                if (hipStreamSynchronize(st) == hipSuccess &&
+                                    hipMemcpyFromSymbol(d.data(), HIP_SYMBOL(g_unit_diag), d.size() * 4) == hipSuccess &&
+                                    ndump < 64) {
+                                        char name[64];
+                                        std::snprintf(name, sizeof name, "gpurun_out/unit_diag_%d.bin", ndump++);
+                                        if (FILE *f = std::fopen(name, "wb")) {
+                                                std::fwrite(d.data(), 4, d.size(), f);
+                                                std::fclose(f);
+                                        }
+                                        if (VRT_LIGHT_DIAG &&
+                                            hipMemcpyFromSymbol(d.data(), HIP_SYMBOL(g_unit_walk), d.size() * 4) == hipSuccess) {
+                                                std::snprintf(name, sizeof name, "gpurun_out/unit_walk_%d.bin", ndump - 1);
+                                                if (FILE *f = std::fopen(name, "wb")) {
+                                                        std::fwrite(d.data(), 4, d.size(), f);
+                                                        std::fclose(f);
+                                                }
+                                        }
+                                }
+                        }
+#endif
                         if (p.test_flags & VRT_TEST_FAIL_LAUNCH)  // test hook: fail between the two launches
                                 return hipErrorLaunchFailure;
                         // the deferred pass only when some ray of the frame may
