@@ -274,16 +274,17 @@ int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
  * every odd chunk of saved rays to its batch-pool launch (the path a chunk
  * with a degenerate ray takes). */
 #define VRT_TEST_STREAM_LEFTOVER 16
-/* VRT_TEST_LIGHT_TAIL makes the light pass hand every sample to its
- * one-ray-per-wave tail launch (the path of samples whose walk passes the
+/* VRT_TEST_LIGHT_TAIL makes the light pass hand every sample to its tail
+ * launch (8 lanes per sample; the path of samples whose walk passes the
  * light pass's triangle-test budget). */
 #define VRT_TEST_LIGHT_TAIL 32
 #define VRT_TEST_VIRTUAL_RANKS_N(n) (VRT_TEST_VIRTUAL_RANKS | ((n) << 8))
 int vrt_set_test_flags(int flags);
 
 /* Diagnostic: the records appended to each compaction queue (phase A, then
- * resume rounds 1..3) by the scene's last config-5 launch; waits for it.
- * All 0 when that launch used no compaction. */
+ * resume rounds 1..3; with the one streaming resume round only queue 0 is
+ * used) by the scene's last config-5 launch; waits for it.  All 0 when that
+ * launch used no compaction. */
 int vrt_secondary_spill_counts(vrt_scene *s, int64_t counts[4]);
 
 /* The kernels' own travorder sort (std::sort of the 8 Items by dist,
