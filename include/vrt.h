@@ -278,6 +278,9 @@ int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
  * launch (8 lanes per sample; the path of samples whose walk passes the
  * light pass's triangle-test budget). */
 #define VRT_TEST_LIGHT_TAIL 32
+/* VRT_TEST_PRIM_TAIL does the same for the primary pass of the cone-traced
+ * render (vrt_render_trace*, vrt_trace_frame_device). */
+#define VRT_TEST_PRIM_TAIL 64
 #define VRT_TEST_VIRTUAL_RANKS_N(n) (VRT_TEST_VIRTUAL_RANKS | ((n) << 8))
 int vrt_set_test_flags(int flags);
 

@@ -693,3 +693,11 @@ def test_trace_main_frame_256_matches_oracle():
     rgb = tree.render_trace(vrt.Camera(*cam), vrt.Film(1, 1, 256, 256), res)
     orgb = osc.render_trace(po.camera(*cam), 1.0, 1.0, 256, 256, res, nthreads=16, samples=False)
     assert np.array_equal(bits(rgb), bits(orgb))
+    # every light-pass and primary-pass sample through the 8-lane tail walks
+    vrt.set_test_flags(vrt.TEST_LIGHT_TAIL | vrt.TEST_PRIM_TAIL)
+    try:
+        assert tree.lightmap(vrt.Camera(*LIGHT), vrt.Film(1, 1, 512, 512)) == hits
+        rgb2 = tree.render_trace(vrt.Camera(*cam), vrt.Film(1, 1, 256, 256), res)
+    finally:
+        vrt.set_test_flags(0)
+    assert np.array_equal(bits(rgb2), bits(orgb))

@@ -711,6 +711,7 @@ TEST_SPILL_ALL = 4  # include/vrt.h VRT_TEST_SPILL_ALL
 TEST_VIRTUAL_RANKS = 8  # include/vrt.h VRT_TEST_VIRTUAL_RANKS (count << 8)
 TEST_STREAM_LEFTOVER = 16  # include/vrt.h VRT_TEST_STREAM_LEFTOVER
 TEST_LIGHT_TAIL = 32  # include/vrt.h VRT_TEST_LIGHT_TAIL
+TEST_PRIM_TAIL = 64  # include/vrt.h VRT_TEST_PRIM_TAIL
 
 
 def set_test_flags(flags):

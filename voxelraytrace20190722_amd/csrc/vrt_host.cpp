@@ -2086,7 +2086,8 @@ static int trace_scratch(vrt_scene *s, int set, const TraceParams &tp, TracePara
                 return VRT_OK;
         TraceSet &t = s->ts[set];
         const size_t nslots = (size_t)tp.r.tiles_this_rank * 256;
-        const size_t need = nslots * 64 + 512;  // the primary pass's 64-B records
+        // the primary pass's 64-B records, its deferred-sample count and list
+        const size_t need = nslots * 64 + 512 + nslots * 4;
         if (t.rec_bytes < need) {
                 if (t.rec) {
                         HIPCHK(hipDeviceSynchronize());  // callers may have queued work on any stream
@@ -2098,6 +2099,8 @@ static int trace_scratch(vrt_scene *s, int set, const TraceParams &tp, TracePara
                 t.rec_bytes = need;
         }
         out->rec = reinterpret_cast<float4 *>(t.rec);
+        out->tail_n = reinterpret_cast<unsigned int *>(static_cast<char *>(t.rec) + nslots * 64);
+        out->tail = reinterpret_cast<uint32_t *>(static_cast<char *>(t.rec) + nslots * 64 + 512);
         return VRT_OK;
 }
 

@@ -469,8 +469,11 @@ struct TraceParams {
         float split_bound[64];
         // split path (rec != nullptr): per-sample records of the primary
         // pass (4 x float4: hit point | hit flag, normal, albedo or sky,
-        // direct light), tiles_this_rank*256 slots, read by k_cones_film
+        // the hit leaf and -d), tiles_this_rank*256 slots, read by k_cones_film
         float4 *rec;
+        // the primary pass's deferred samples (k_trace_prim_tail): count, slots
+        unsigned int *tail_n;
+        uint32_t *tail;
 };
 
 // GPU octree build (vrt_build.hip): the host build's

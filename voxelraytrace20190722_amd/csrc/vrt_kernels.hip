@@ -2928,16 +2928,21 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_resum
         SpillCursor cur;
         cur.chunk = kSpillNone;
         cur.fill = 0;
-        // leftover mode (after k_sec_stream): the chunks it listed, from ctr[4]
+        // leftover mode (after k_sec_stream): the chunks it listed, from ctr[4],
+        // each as kSpillChunk / 64 pieces of 64 rays on different waves (the
+        // few leftover chunks of a frame would otherwise leave one wave
+        // walking a whole chunk's batches one after the other)
         const bool left = VRT_SEC_POOL_RESUME && p.sq.stream;
-        const uint32_t nl = left ? p.sq.ctr[3] : 0u;
+        constexpr uint32_t kParts = kSpillChunk / 64;
+        const uint32_t nl = left ? p.sq.ctr[3] * kParts : 0u;
         for (;;) {
-                uint32_t c;
+                uint32_t c, part = 0;
                 if (left) {
                         const uint32_t j = take_n(p.sq.ctr + 4, 1u);
                         if (j >= nl)
                                 break;
-                        c = __builtin_amdgcn_readfirstlane(p.sq.fill[1][j]);
+                        c = __builtin_amdgcn_readfirstlane(p.sq.fill[1][j / kParts]);
+                        part = j % kParts;
                 } else {
                         c = take_n(cin + 1, 1u);
                         if (c >= n)
@@ -2945,8 +2950,12 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_resum
                 }
                 if (VRT_SEC_POOL_RESUME) {
                         const int w = VRT_SEC_POOL_RESUME ? tid >> 6 : 0;
-                        resume_pool_chunk<kR64>(p, in + (size_t)c * kSpillChunk, fin[c], stk + tid, dirs[w], opix[w],
-                                                mbox[w], hword + (tid >> 6));
+                        const uint32_t f = fin[c], lo = part * 64u;
+                        if (lo >= f)
+                                continue;
+                        const uint32_t cnt = left ? min(64u, f - lo) : f;
+                        resume_pool_chunk<kR64>(p, in + (size_t)c * kSpillChunk + lo, cnt, stk + tid, dirs[w],
+                                                opix[w], mbox[w], hword + (tid >> 6));
                 } else {
                         resume_chunk<kR64>(p, in + (size_t)c * kSpillChunk, fin[c], t, cur, stk + tid);
                 }
@@ -4376,21 +4385,26 @@ __global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
 // ---- split trace: primary pass, one lane per (sample, cone), film add ----
 // Primary pass: trace()'s ray_march + get_albedo + leaf compute_illum(-d);
 // slot = work unit * kRenderBlock + tid.
-template <bool kR64>
-__device__ __forceinline__ void trace_prim_unit(const TraceParams &p, uint2 *stk, int u)
+// The primary pass's walks can be budgeted as the light pass's
+// (VRT_LIGHT_BUDGET): a sample past VRT_PRIM_BUDGET triangle tests is
+// re-walked by k_trace_prim_tail with a group of lanes, which writes its
+// record.  Off by default: the view's long walks are not a few waves'
+// tail as the light pass's are, and the re-walks cost more than they save
+// (VRT_TEST_PRIM_TAIL still runs the tail path in the tests).
+#ifndef VRT_PRIM_BUDGET
+#define VRT_PRIM_BUDGET 0  // off: 256 / 128 / 512 measured -11 / -21 / -3.5 % on the render (the view's deferred samples are many)
+#endif
+__device__ __forceinline__ RayK trace_ray(const TraceParams &p, int px, int py, int s)
 {
-        const int tid = threadIdx.x;
-        int k, px, py, s, lx, ly;
-        if (!tile_lane(p.r, u, k, px, py, s, lx, ly))
-                return;
-        const int64_t slot = (int64_t)u * kRenderBlock + tid;
         const CamParams &c = p.r.cam;
         const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
                                  sample_x(s), sample_y(s));
-        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
-                                 dn, c.tmin, c.tmax);
-        MarchResult m;
-        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
+        return make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]), dn, c.tmin, c.tmax);
+}
+
+__device__ __forceinline__ void trace_prim_record(const TraceParams &p, const RayK &r, const MarchResult &m,
+                                                  int64_t slot)
+{
         float4 *o = p.rec + 4 * slot;
         if (m.hit) {
                 f3 nrm;
@@ -4411,10 +4425,58 @@ __device__ __forceinline__ void trace_prim_unit(const TraceParams &p, uint2 *stk
 }
 
 template <bool kR64>
+__device__ __forceinline__ void trace_prim_unit(const TraceParams &p, uint2 *stk, int u)
+{
+        const int tid = threadIdx.x;
+        int k, px, py, s, lx, ly;
+        if (!tile_lane(p.r, u, k, px, py, s, lx, ly))
+                return;
+        const int64_t slot = (int64_t)u * kRenderBlock + tid;
+        const RayK r = trace_ray(p, px, py, s);
+        MarchResult m;
+        if (p.r.test_flags & VRT_TEST_PRIM_TAIL)
+                m.deferred = true;  // test hook: every sample to k_trace_prim_tail
+        else
+                ray_march_dispatch<false, kRenderBlock, 1, kR64, 0, VRT_PRIM_BUDGET>(p.r.sc, r, stk + tid, nullptr,
+                                                                                    nullptr, m);
+        if (m.deferred) {
+                const uint32_t j = atomicAdd(p.tail_n, 1u);
+                p.tail[j] = (uint32_t)slot;
+                return;
+        }
+        trace_prim_record(p, r, m, slot);
+}
+
+template <bool kR64>
 __global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
         trace_prim_unit<kR64>(p, stk, chunk_place<VRT_PRIM_CHUNK>(blockIdx.x, gridDim.x));
+}
+
+// The primary pass's deferred samples, one per group of VRT_LIGHT_TAIL_G
+// lanes (as k_light_tail): the group re-walks the sample from the root and
+// its first lane writes the sample's record.
+template <bool kR64>
+__global__ __launch_bounds__(64) void k_trace_prim_tail(TraceParams p)
+{
+        constexpr int kG = VRT_LIGHT_TAIL_G, kR = 64 / kG;
+        __shared__ uint2 stk[kStack * 64];
+        const uint32_t n = *p.tail_n;
+        for (uint32_t i0 = blockIdx.x * kR; i0 < n; i0 += gridDim.x * kR) {
+                const uint32_t i = i0 + threadIdx.x / kG;
+                if (i < n) {  // whole groups
+                        const uint32_t slot = p.tail[i];
+                        int k, px, py, s, lx, ly;
+                        tile_lane_at(p.r, (int)(slot / kRenderBlock), (int)(slot % kRenderBlock), k, px, py, s, lx,
+                                     ly);
+                        const RayK r = trace_ray(p, px, py, s);
+                        MarchResult m;
+                        ray_march_dispatch<false, 64, kG, kR64>(p.r.sc, r, stk + threadIdx.x, nullptr, nullptr, m);
+                        if ((threadIdx.x & (kG - 1)) == 0)
+                                trace_prim_record(p, r, m, slot);
+                }
+        }
 }
 
 // Cones + film: one wave per work unit of the primary pass (its 64 sample
@@ -4578,8 +4640,15 @@ hipError_t launch_trace_prim(const TraceParams &p, hipStream_t st)
 {
         if (p.r.tiles_this_rank <= 0)
                 return hipSuccess;
+        const bool tail = VRT_PRIM_BUDGET > 0 || (p.r.test_flags & VRT_TEST_PRIM_TAIL);
+        if (tail)
+                if (hipError_t e = hipMemsetAsync(p.tail_n, 0, 4, st))
+                        return e;
         hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace_prim<true> : k_trace_prim<false>,
                            dim3(trace_vblocks(p.r.tiles_this_rank)), dim3(kRenderBlock), 0, st, p);
+        if (tail)
+                hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace_prim_tail<true> : k_trace_prim_tail<false>,
+                                   dim3(VRT_LIGHT_TAIL_GRID), dim3(64), 0, st, p);
         return hipGetLastError();
 }
 
