@@ -2897,8 +2897,11 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
 
 // The streaming resume round (VRT_SEC_STREAM, films under 2^26 pixels): one
 // resident generation, each wave one stream (resume_stream) over queue 0.
+#ifndef VRT_STREAM_WAVES_PER_EU
+#define VRT_STREAM_WAVES_PER_EU VRT_SECP_WAVES_PER_EU
+#endif
 template <bool kR64>
-__global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_stream(ResumeParams p)
+__global__ __launch_bounds__(kSecPBlock, VRT_STREAM_WAVES_PER_EU) void k_sec_stream(ResumeParams p)
 {
         __shared__ uint2 stk[kStack * kSecPBlock];
         __shared__ float dirs[kSecPBlock / 64][64][3];
@@ -3017,7 +3020,7 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
 }
 
 #ifndef VRT_SEC_SPILL_T
-#define VRT_SEC_SPILL_T 24    // phase A stops below this many walking lanes (0: no compaction)
+#define VRT_SEC_SPILL_T 12    // phase A stops below this many walking lanes (0: no compaction); round 4 with the streaming resume: 8 / 12 / 16 / 20 / 24 / 32 / 48 = 18.07 / 17.21 / 17.28 / 17.54 / 17.65 / 17.66 / 17.83 ms
 #endif
 #ifndef VRT_SEC_SPILL_T2
 #define VRT_SEC_SPILL_T2 24   // the same in resume rounds before the last
