@@ -4493,7 +4493,7 @@ __global__ __launch_bounds__(64) void k_trace_prim_tail(TraceParams p)
 // pixel is written once: each sample record is read once, and no per-cone
 // result goes through memory.
 #ifndef VRT_CONES_WAVES_PER_EU
-#define VRT_CONES_WAVES_PER_EU 8  // 64 VGPRs, 24 B/lane of spill outside the step loop (7 waves: 70, none, -0.7 %)
+#define VRT_CONES_WAVES_PER_EU 7  // 70 VGPRs, no spill: +9.8 % over 8 waves (64 VGPRs, 36 B/lane of spill once the direct term moved here; round 4)
 #endif
 __global__ __launch_bounds__(64, VRT_CONES_WAVES_PER_EU) void k_cones_film(TraceParams p)
 {
