@@ -3787,8 +3787,11 @@ __device__ __forceinline__ void light_unit(const LightParams &p, uint2 *stk, int
                 light_record(p, r, m, px, py, s);
 }
 
+#ifndef VRT_LIGHT_WAVES_PER_EU
+#define VRT_LIGHT_WAVES_PER_EU 6  // 80 VGPRs (the compiler alone: 98, 4 waves); light map +2 %, round 4
+#endif
 template <bool kR64>
-__global__ __launch_bounds__(kRenderBlock) void k_light(LightParams p)
+__global__ __launch_bounds__(kRenderBlock, VRT_LIGHT_WAVES_PER_EU) void k_light(LightParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
         light_unit<kR64>(p, stk, chunk_place<VRT_LIGHT_CHUNK>(blockIdx.x, gridDim.x));
@@ -4450,8 +4453,11 @@ __device__ __forceinline__ void trace_prim_unit(const TraceParams &p, uint2 *stk
         trace_prim_record(p, r, m, slot);
 }
 
+#ifndef VRT_PRIM_WAVES_PER_EU
+#define VRT_PRIM_WAVES_PER_EU 1  // 1: the compiler's choice
+#endif
 template <bool kR64>
-__global__ __launch_bounds__(kRenderBlock) void k_trace_prim(TraceParams p)
+__global__ __launch_bounds__(kRenderBlock, VRT_PRIM_WAVES_PER_EU) void k_trace_prim(TraceParams p)
 {
         __shared__ uint2 stk[kStack * kRenderBlock];
         trace_prim_unit<kR64>(p, stk, chunk_place<VRT_PRIM_CHUNK>(blockIdx.x, gridDim.x));
