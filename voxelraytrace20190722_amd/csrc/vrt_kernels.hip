@@ -3804,8 +3804,11 @@ __global__ __launch_bounds__(kRenderBlock, VRT_LIGHT_WAVES_PER_EU) void k_light(
 #ifndef VRT_LIGHT_TAIL_G
 #define VRT_LIGHT_TAIL_G 8
 #endif
+#ifndef VRT_TAIL_WAVES_PER_EU
+#define VRT_TAIL_WAVES_PER_EU 1  // 1: the compiler's choice
+#endif
 template <bool kR64>
-__global__ __launch_bounds__(64) void k_light_tail(LightParams p)
+__global__ __launch_bounds__(64, VRT_TAIL_WAVES_PER_EU) void k_light_tail(LightParams p)
 {
         constexpr int kG = VRT_LIGHT_TAIL_G, kR = 64 / kG;  // lanes per sample, samples per wave
         __shared__ uint2 stk[kStack * 64];
