@@ -78,18 +78,18 @@ oracle:
 
 # A/B variant of the kernels:  make variant NAME=v0 DEFS="-DVRT_EXPAND_V=0"
 variant: $(HOSTOBJS) $(BLD)/vrt_build.o | $(BLD)
-	mkdir -p build/variants
-	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
-	  build/variants/k_$(NAME).o $(BLD)/vrt_build.o $(HOSTOBJS) $(BLD)/vrt_build_id.o $(LIBS)
+	mkdir -p build/ab
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/ab/k_$(NAME).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/ab/libvrt_$(NAME).so \
+	  build/ab/k_$(NAME).o $(BLD)/vrt_build.o $(HOSTOBJS) $(BLD)/vrt_build_id.o $(LIBS)
 
 # variant that also rebuilds the host side (for data-layout changes)
 fullvariant: $(BLD)/vrt_build.o $(BLD)/vrt_legacy.o $(BLD)/vrt_multi.o $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o | $(BLD)
-	mkdir -p build/variants
-	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/variants/k_$(NAME).o
-	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_host.cpp -o build/variants/h_$(NAME).o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/libvrt_$(NAME).so \
-	  build/variants/k_$(NAME).o build/variants/h_$(NAME).o $(BLD)/vrt_build.o $(BLD)/vrt_legacy.o $(BLD)/vrt_multi.o \
+	mkdir -p build/ab
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(DEFS) -c $(SRC)/vrt_kernels.hip -o build/ab/k_$(NAME).o
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/vrt_host.cpp -o build/ab/h_$(NAME).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/ab/libvrt_$(NAME).so \
+	  build/ab/k_$(NAME).o build/ab/h_$(NAME).o $(BLD)/vrt_build.o $(BLD)/vrt_legacy.o $(BLD)/vrt_multi.o \
 	  $(BLD)/vrt_hdr.o $(BLD)/vrt_proxy.o $(BLD)/vrt_obj.o $(BLD)/vrt_tga.o $(BLD)/vrt_build_id.o $(LIBS)
 
 # ISA listing + register/occupancy report of the kernels (for DESIGN.md)

@@ -391,9 +391,10 @@ def parse():
     p.add_argument("--frames-in-flight", type=int, default=3,
                    help="consecutive frames on this many HIP streams (own output buffers), so a frame's "
                         "ramp-down overlaps the next frame's launch; 1 = one stream")
-    p.add_argument("--rehearse-rank", type=int, default=0,
+    p.add_argument("--rehearse-rank", type=int, default=-1,
                    help="with --rehearse-ranks: whose share to render (0: rank 0, which also gathers and "
-                        "unpacks; from 4 ranks on the deal gives it fewer tiles than the others)")
+                        "unpacks; from 4 ranks on the deal gives it fewer tiles than the others; -1 (default): "
+                        "every rank's in turn, the reported step = the slowest rank's)")
     p.add_argument("--rehearse-render-only", action="store_true",
                    help="with --rehearse-ranks: time the share's renders alone (no gather, no unpack)")
     p.add_argument("--frames-in-flight-trace", type=int, default=1,
@@ -686,7 +687,10 @@ def main():
         if k is not None:
             ev_coll[k].record(s)
             coll_done.append(k)
-        if rank == 0:  # each buffer slot re-assembles into its own image (frames in flight)
+        # rank 0 re-assembles (each buffer slot into its own image: frames in
+        # flight); a rehearsal of rank r >= 1's share does what that rank
+        # does -- render + gather send, no unpack
+        if rank == 0 and not (rehearse and cur["share"] != 0):
             if k is not None:
                 ev_unp[k][0].record(s)
             if secondary:
@@ -755,7 +759,7 @@ def main():
                 ev[k][1].record(s)
             return
         finish(b, s)  # frame k - nbuf used this buffer pair (normally finished already)
-        render(cam, a.rehearse_rank if rehearse else rank, nshare, 0, tiles[b].data_ptr(), s)
+        render(cam, cur["share"], nshare, 0, tiles[b].data_ptr(), s)
         if timed:
             ev[k][1].record(s)
         if rehearse and a.rehearse_render_only:
@@ -781,31 +785,64 @@ def main():
         for b in range(nbuf):
             finish(b, stream)
 
-    for k in range(a.warmup):
-        step(k, False)
-    drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for k in range(a.steps):
-        step(k, True)
-    drain()
-    # host time to enqueue the K steps: close to `elapsed` means the host
-    # loop, not the GPU, sets the pace
-    host_enq = time.perf_counter() - t_start
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    elapsed_local = elapsed
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kms = np.array([s.elapsed_time(e) for s, e in ev])  # render launch span (HIP events on its stream), ms
+    def timed_run():
+        """W warm-up steps, then K timed steps between barrier + synchronize
+        -> (max-over-ranks elapsed s, this rank's elapsed s, host enqueue s)"""
+        coll_done.clear()
+        unp_done.clear()
+        for k in range(a.warmup):
+            step(k, False)
+        drain()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        for k in range(a.steps):
+            step(k, True)
+        drain()
+        # host time to enqueue the K steps: close to `elapsed` means the host
+        # loop, not the GPU, sets the pace
+        host_enq = time.perf_counter() - t_start
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t_start
+        elapsed_local = elapsed
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, elapsed_local, host_enq
+
+    # the share a step renders: this rank's, or in a rehearsal the rehearsed
+    # rank's (--rehearse-rank -1: every rank's in turn, the step = the
+    # slowest, as an N-GPU step waits for its slowest rank)
+    cur = {"share": rank}
+    reh_rows = []
+    if rehearse:
+        order = list(range(nshare)) if a.rehearse_rank < 0 else [a.rehearse_rank]
+        runs = []
+        for r_ in order:
+            cur["share"] = r_
+            el_, ell_, he_ = timed_run()
+            kms_ = np.array([s.elapsed_time(e) for s, e in ev])
+            coll_ = float(np.mean([ev[k][1].elapsed_time(ev_coll[k]) for k in coll_done])) if coll_done else 0.0
+            unp_ = float(np.mean([ev_unp[k][0].elapsed_time(ev_unp[k][1]) for k in unp_done])) if unp_done else 0.0
+            runs.append((el_, ell_, he_, kms_, coll_, unp_))
+            reh_rows.append({"share_of_rank": r_, "ms_per_step": round(el_ * 1e3 / a.steps, 4),
+                             "share_render_ms": round(float(kms_.mean()), 4), "collective_ms": round(coll_, 4),
+                             "unpack_ms": round(unp_, 4), "host_enqueue_ms_per_step": round(he_ * 1e3 / a.steps, 4)})
+            log(f"[rehearsal] rank {r_}'s share: {el_ * 1e3 / a.steps:.4f} ms per step")
+        worst = max(range(len(runs)), key=lambda i: runs[i][0])
+        elapsed, elapsed_local, host_enq, kms_w, _, _ = runs[worst]
+        cur["share"] = order[worst]
+        coll_w, unp_w = runs[worst][4], runs[worst][5]
+    else:
+        elapsed, elapsed_local, host_enq = timed_run()
+    # render launch span (HIP events on its stream), ms
+    kms = kms_w if rehearse else np.array([s.elapsed_time(e) for s, e in ev])
     if trace:  # the light map alone (blocking build), for reference beside the overlapped frame
         for _ in range(4):
             torch.cuda.synchronize()
@@ -814,14 +851,18 @@ def main():
             light_ms.append((time.perf_counter() - t0_) * 1e3)
     per_rank = None
     if world > 1 or (rehearse and not a.rehearse_render_only):
-        coll_ms = float(np.mean([ev[k][1].elapsed_time(ev_coll[k]) for k in coll_done])) if coll_done else 0.0
-        unp_ms = float(np.mean([ev_unp[k][0].elapsed_time(ev_unp[k][1]) for k in unp_done])) if unp_done else 0.0
+        if rehearse:
+            coll_ms, unp_ms = coll_w, unp_w
+        else:
+            coll_ms = float(np.mean([ev[k][1].elapsed_time(ev_coll[k]) for k in coll_done])) if coll_done else 0.0
+            unp_ms = float(np.mean([ev_unp[k][0].elapsed_time(ev_unp[k][1]) for k in unp_done])) if unp_done else 0.0
         vals = [float(kms.mean()), coll_ms, unp_ms, elapsed_local]
         if world > 1:
             per_rank = per_rank_report(world, a.dist_backend, dev, rank, vals)
             seen = ranks_seen(a.dist_backend, dev)
         else:
-            per_rank = [{"rank": 0, **{k_: round(v_, 4) for k_, v_ in zip(RANK_FIELDS, vals)}}]
+            per_rank = [{"rank": 0, "share_of_rank": cur["share"],
+                         **{k_: round(v_, 4) for k_, v_ in zip(RANK_FIELDS, vals)}}]
     # per-frame device time: the launch span with one frame in flight; with
     # several, spans overlap (a span also holds the wait for the CUs the
     # previous frame still occupies), so the frame time is the step time
@@ -1182,15 +1223,21 @@ def main():
             # the RCCL call sequence, on one GPU; the xGMI transfer is absent
             out["metric"] = "rehearsal: " + metric
             out["value"] = None
-            out["config"]["parallelism"] = (f"rank {a.rehearse_rank}'s share of {nshare} screen-tile shares + "
+            who = "every rank's share in turn (step = the slowest)" if a.rehearse_rank < 0 else \
+                f"rank {a.rehearse_rank}'s share"
+            out["config"]["parallelism"] = (f"{who} of {nshare} screen-tile shares + "
                                             f"rccl gather (1-rank group)")
             out["rehearsal"] = {
-                "ranks": nshare, "share_of_rank": a.rehearse_rank, "frames_per_s": round(a.steps / elapsed, 2),
+                "ranks": nshare, "share_of_rank": cur["share"],
+                "shares_rehearsed": [r_["share_of_rank"] for r_ in reh_rows],
+                "step_is": "max over the rehearsed ranks' steps" if len(reh_rows) > 1 else "the one rehearsed rank's step",
+                "per_rank": reh_rows,
+                "frames_per_s": round(a.steps / elapsed, 2),
                 "projected_Mrays_per_s_without_xgmi": round(value, 2),
                 "share_kernel_ms_mean": round(float(kms.mean()), 4),
-                "note": "per-rank step time of the N-rank path (render of 1/N of the tiles, RCCL gather, unpack "
-                        "of N rank buffers, Python host loop) on one GPU; a real N-GPU step adds the xGMI "
-                        "transfer into rank 0"}
+                "note": "per-rank step of the N-rank path on one GPU, each rank's share in turn doing what that rank "
+                        "does: render of its tiles + RCCL gather (1-rank group: no xGMI transfer) + on rank 0 the "
+                        "unpack of N rank buffers; a real N-GPU step adds the xGMI transfer into rank 0"}
             out["kernel_mrays_per_s"] = round(mean_rays / nshare / (frame_ms * 1e-3) / 1e6, 2)
         out["build_id"] = vrt.build_id()
         print(json.dumps(out), flush=True)

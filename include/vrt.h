@@ -283,6 +283,8 @@ int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
 #define VRT_TEST_PRIM_TAIL 64
 #define VRT_TEST_VIRTUAL_RANKS_N(n) (VRT_TEST_VIRTUAL_RANKS | ((n) << 8))
 int vrt_set_test_flags(int flags);
+/* The current vrt_set_test_flags value (so a caller can restore it). */
+int vrt_test_flags(void);
 
 /* Diagnostic: the records appended to each compaction queue (phase A, then
  * resume rounds 1..3; with the one streaming resume round only queue 0 is
@@ -433,6 +435,11 @@ int stbi_write_hdr(char const *filename, int w, int h, int comp,
 /* Source hash this library was built from (tools/build_id.py: sha256 of
  * csrc/, include/vrt.h and the Makefile, 16 hex digits). */
 const char *vrt_build_id(void);
+/* The value of one path-selecting compile-time switch of this build (e.g.
+ * "VRT_SEC_SPILL_T": config 5's compaction threshold, 0 = no compaction;
+ * "VRT_SEC_STREAM": the streaming resume round); VRT_E_INVALID for a name the
+ * build does not know.  Lets a test assert which path a build takes. */
+int vrt_build_flag(const char *name, int64_t *value);
 
 /* ---- scene ingest (VRT/voxel_octree.cc:305-388) -------------------------
  * vrt_obj_load = obj2voxel(path) + load_image for every texture a face

@@ -126,7 +126,12 @@ def test_c5_1080p_depth8_secondary_whole_frame(proxy):
                                        nthreads=NTH, ids=False)
     assert rays == orays > 1920 * 1080 * 32
     assert np.array_equal(bits(vis), bits(ovis))
-    assert sum(counts) >= 0  # > 0 in a compaction build (VRT_SEC_COOP=0); the pooled walk keeps no queues
+    # the default build compacts (VRT_SEC_SPILL_T > 0) and streams the saved
+    # rays (VRT_SEC_STREAM): phase A stopped rays, and the one streaming round
+    # left queue 1 empty -- a build with the compaction off fails here
+    assert vrt.build_flag("VRT_SEC_SPILL_T") > 0 and vrt.build_flag("VRT_SEC_STREAM") == 1
+    assert counts[0] > 0, counts
+    assert counts[1:] == [0, 0, 0], counts
     prim = torch.zeros(1920 * 1080 * 8, dtype=torch.float32, device="cuda:0")
     dvis = torch.zeros((1080, 1920), dtype=torch.float32, device="cuda:0")
     tree.render_secondary_device(cam, film, 64, 0, 1, prim.data_ptr(), dvis.data_ptr(), None)

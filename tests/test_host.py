@@ -325,6 +325,30 @@ def test_scene_nodes_and_build_flags():
         vrt.VoxelOctree(sd, 6, device=-1, build_on_device=True)
 
 
+def test_kernel_build_flags_are_the_defaults():
+    """vrt_build_flag reports the kernel build's path switches; the tested
+    build is the production one (config 5 compacts and streams, persistent
+    fast-only primary render); unknown names are rejected."""
+    assert vrt.build_flag("VRT_SEC_SPILL_T") > 0
+    assert vrt.build_flag("VRT_SEC_STREAM") == 1
+    assert vrt.build_flag("VRT_PERSIST") == 1 and vrt.build_flag("VRT_PERSIST_FAST") == 1
+    assert vrt.build_flag("VRT_NODE_BOX") == 1
+    with pytest.raises(vrt.VrtError):
+        vrt.build_flag("VRT_NO_SUCH_FLAG")
+
+
+def test_test_flags_round_trip():
+    """vrt_test_flags reads back vrt_set_test_flags; MultiOctree's virtual
+    ranks restore the caller's flags."""
+    prev = vrt.test_flags()
+    try:
+        vrt.set_test_flags(vrt.TEST_SPILL_ALL | vrt.TEST_LIGHT_TAIL)
+        assert vrt.test_flags() == vrt.TEST_SPILL_ALL | vrt.TEST_LIGHT_TAIL
+    finally:
+        vrt.set_test_flags(prev)
+    assert vrt.test_flags() == prev
+
+
 def test_build_id_matches_tree():
     """libvrt.so was built from the sources in this tree (tools/build_id.py)."""
     import build_id

@@ -49,6 +49,14 @@ def main():
                     help="primary mode: time every rank's share of an N-rank frame separately (launch by launch; "
                          "per pose the slowest rank counts, as in an N-GPU step), images re-assembled with each "
                          "variant's own vrt_unpack_tiles_device for the parity check")
+    ap.add_argument("--share-ranks", type=int, default=0,
+                    help="primary mode: time rank shares of an N-rank frame as the rehearsal runs them -- K "
+                         "frames of one rank's share with frames in flight (--fl streams), wall clock per step; "
+                         "the variant's figure is the max over --share-of ranks (an N-GPU step waits for the "
+                         "slowest rank)")
+    ap.add_argument("--share-of", default="0,1", help="ranks whose shares --share-ranks times")
+    ap.add_argument("--fl", type=int, default=3, help="--share-ranks: frames in flight")
+    ap.add_argument("--steps", type=int, default=64, help="--share-ranks: frames per timed run")
     a = ap.parse_args()
     tr = a.mode == "trace"
     a.width = a.width or (1024 if tr else 1920)
@@ -75,6 +83,8 @@ def main():
         libs[0].vrt_camera_init(fov, eye.ctypes.data_as(_ffi.f32p), spot.ctypes.data_as(_ffi.f32p),
                                 up.ctypes.data_as(_ffi.f32p), 0.0, vrt.FLT_MAX, C.byref(cam))
         cams.append(cam)
+    if a.share_ranks > 1:
+        return share_ab(a, libs, scenes, film, cams)
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream(dev)
     sec = a.mode == "secondary"
@@ -146,6 +156,63 @@ def main():
         out[os.path.basename(p)] = {"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
                                     "speedup": round(float(base / np.median(t)), 3),
                                     "mrays": round(a.width * a.height * 4 / np.median(t) / 1e3, 1)}
+    print(json.dumps(out, indent=1))
+
+
+def share_ab(a, libs, scenes, film, cams):
+    """--share-ranks R: per variant and round, K frames of rank r's share of
+    an R-rank frame (the pose sweep, frames in flight on --fl streams, each
+    frame its own packed buffer), wall clock around them; per rank the median
+    over rounds, the variant's figure the max over the ranks.  Parity: every
+    rank's share of the last pose re-assembled and compared with the first
+    variant's image."""
+    dev = torch.device("cuda:0")
+    R, F = a.share_ranks, a.fl
+    ranks = [int(x) for x in a.share_of.split(",")]
+    streams = [torch.cuda.Stream(dev) for _ in range(F)]
+    tpr = [L.vrt_tiles_per_rank(C.byref(film), R) for L in libs]
+    packs = [torch.zeros((max(F, R), t * 192), dtype=torch.float32, device=dev) for t in tpr]
+    img = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev)
+    for L, h in zip(libs, scenes):
+        assert L.vrt_scene_set_frames_in_flight(h, F) == 0, L.vrt_last_error()
+    ref = None
+    times = {p: {r: [] for r in ranks} for p in a.libs}
+    for rd in range(a.rounds + 1):
+        for vi, (L, h, p) in enumerate(zip(libs, scenes, a.libs)):
+            if rd == 0:  # warm-up + parity: every rank's share of the last pose
+                s0 = streams[0].cuda_stream
+                for rk in range(R):
+                    rc = L.vrt_render_tiles_device(h, C.byref(cams[-1]), C.byref(film), rk, R, 0,
+                                                   C.c_void_p(packs[vi][rk].data_ptr()), C.c_void_p(s0))
+                    assert rc == 0, L.vrt_last_error()
+                L.vrt_unpack_tiles_device(C.byref(film), R, C.c_void_p(packs[vi].data_ptr()),
+                                          C.c_void_p(img.data_ptr()), C.c_void_p(s0))
+                torch.cuda.synchronize()
+                im = img.cpu().numpy().view(np.uint32)
+                if ref is None:
+                    ref = im
+                elif not a.no_check and not np.array_equal(im, ref):
+                    raise SystemExit(f"variant {p} differs from baseline {a.libs[0]}")
+                continue
+            for rk in ranks:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for k in range(a.steps):
+                    s = streams[k % F]
+                    rc = L.vrt_render_tiles_device(h, C.byref(cams[k % len(cams)]), C.byref(film), rk, R, 0,
+                                                   C.c_void_p(packs[vi][k % F].data_ptr()),
+                                                   C.c_void_p(s.cuda_stream))
+                    assert rc == 0, L.vrt_last_error()
+                torch.cuda.synchronize()
+                times[p][rk].append((time.perf_counter() - t0) * 1e3 / a.steps)
+    out = {}
+    base = None
+    for p in a.libs:
+        per = {r: float(np.median(times[p][r])) for r in ranks}
+        mx = max(per.values())
+        base = base or mx
+        out[os.path.basename(p)] = {"max_step_ms": round(mx, 4), "speedup": round(base / mx, 3),
+                                    "per_rank_ms": {r: round(v, 4) for r, v in per.items()}}
     print(json.dumps(out, indent=1))
 
 

@@ -5,14 +5,14 @@
 #   make variant NAME=<name> DEFS="-D..."       (kernels only)
 #   make fullvariant NAME=<name> DEFS="-D..."   (kernels + host side)
 # usage: tools/ab_call.sh [--sets d8,d9,4k,sec,r8,d6,tr] NAME1 NAME2 ...
-#        (build/variants/libvrt_NAME.so; "head" = the in-tree libvrt.so)
+#        (build/ab/libvrt_NAME.so; "head" = the in-tree libvrt.so)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 sets="d8,4k,sec"
 if [ "$1" = "--sets" ]; then sets=$2; shift 2; fi
 L=""
 for n in "$@"; do
-  if [ "$n" = head ]; then L="$L voxelraytrace20190722_amd/libvrt.so"; else L="$L build/variants/libvrt_$n.so"; fi
+  if [ "$n" = head ]; then L="$L voxelraytrace20190722_amd/libvrt.so"; else L="$L build/ab/libvrt_$n.so"; fi
 done
 steps=()
 for s in ${sets//,/ }; do
@@ -23,6 +23,7 @@ for s in ${sets//,/ }; do
     sec) steps+=("ab_sec|400|python -u tools/ab.py $L --mode secondary --poses 8 --rounds 3") ;;
     r8)  steps+=("ab_r8|300|python -u tools/ab.py $L --ranks 8 --rounds 4") ;;
     tr)  steps+=("ab_tr|300|python -u tools/ab.py $L --mode trace --rounds 4") ;;
+    s8)  steps+=("ab_s8|400|python -u tools/ab.py $L --share-ranks 8 --share-of 0,1,4 --rounds 5 --steps 64") ;;
     d6)  steps+=("ab_d6|300|python -u tools/ab.py $L --depth 6 --rounds 4") ;;
     *) echo "unknown set $s"; exit 2 ;;
   esac

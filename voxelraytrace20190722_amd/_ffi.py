@@ -121,6 +121,8 @@ SIGNATURES = {
     "vrt_write_hdr": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, f32p]),
     "stbi_write_hdr": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, f32p]),
     "vrt_build_id": (C.c_char_p, []),
+    "vrt_build_flag": (C.c_int, [C.c_char_p, i64p]),
+    "vrt_test_flags": (C.c_int, []),
     "vrt_set_test_flags": (C.c_int, [C.c_int]),
     "vrt_camera_defer_bound": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]),
     "vrt_secondary_spill_counts": (C.c_int, [_P, i64p]),

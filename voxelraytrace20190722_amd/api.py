@@ -506,11 +506,13 @@ class MultiOctree:
         d = scene.desc()
         flags = _ffi.VRT_BUILD_DEVICE if build_on_device else 0
         if virtual_ranks:
-            lib().vrt_set_test_flags(TEST_VIRTUAL_RANKS | (int(virtual_ranks) << 8))
+            prev = lib().vrt_test_flags()  # restored afterwards: a caller's own test flags stay set
+            lib().vrt_set_test_flags((prev & 0xFF & ~TEST_VIRTUAL_RANKS) | TEST_VIRTUAL_RANKS
+                                     | (int(virtual_ranks) << 8))
             try:
                 rc = lib().vrt_scene_create_multi(C.byref(d), int(max_depth), int(device_mask), flags, C.byref(h))
             finally:
-                lib().vrt_set_test_flags(0)
+                lib().vrt_set_test_flags(prev)
         else:
             rc = lib().vrt_scene_create_multi(C.byref(d), int(max_depth), int(device_mask), flags, C.byref(h))
         check(rc, "vrt_scene_create_multi")
@@ -705,6 +707,15 @@ def build_id():
     return lib().vrt_build_id().decode()
 
 
+def build_flag(name):
+    """A path-selecting compile-time switch of libvrt.so's kernel build
+    (vrt_build_flag), e.g. "VRT_SEC_SPILL_T" (config 5's compaction
+    threshold; 0 = no compaction)."""
+    v = C.c_int64()
+    check(lib().vrt_build_flag(name.encode(), C.byref(v)), "vrt_build_flag")
+    return v.value
+
+
 TEST_FORCE_DEFER = 1  # include/vrt.h VRT_TEST_FORCE_DEFER
 TEST_FAIL_LAUNCH = 2  # include/vrt.h VRT_TEST_FAIL_LAUNCH
 TEST_SPILL_ALL = 4  # include/vrt.h VRT_TEST_SPILL_ALL
@@ -717,6 +728,11 @@ TEST_PRIM_TAIL = 64  # include/vrt.h VRT_TEST_PRIM_TAIL
 def set_test_flags(flags):
     """Test hook (vrt_set_test_flags): flags read by every later launch."""
     check(lib().vrt_set_test_flags(int(flags)), "vrt_set_test_flags")
+
+
+def test_flags():
+    """The current vrt_set_test_flags value (vrt_test_flags)."""
+    return int(lib().vrt_test_flags())
 
 
 def device_count():

@@ -1027,9 +1027,19 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                 (void)hipSetDevice(s->device);
                 if (s->stream)
                         (void)hipStreamSynchronize(s->stream);
+                // launches on callers' streams: every work-queue slot, trace
+                // set and compaction set records its last user's event
+                for (int k = 0; k < kQueueSlots; ++k)
+                        if (s->q_live[k])
+                                (void)hipEventSynchronize(s->q_ev[k]);
+                for (TraceSet &t : s->ts)
+                        if (t.live)
+                                (void)hipEventSynchronize(t.ev);
+                for (int k = 0; k < 2; ++k)
+                        if (s->spill_live[k])
+                                (void)hipEventSynchronize(s->spill_ev[k]);
                 if (s->d_mem)
                         (void)hipFree(s->d_mem);
-                (void)hipDeviceSynchronize();  // trace frames run on callers' streams too
                 for (TraceSet &t : s->ts) {
                         if (t.lm)
                                 (void)hipFree(t.lm);
@@ -1219,6 +1229,17 @@ extern "C" int vrt_set_test_flags(int flags)
 
 int vrt::test_flags() { return g_test_flags.load(); }
 
+extern "C" int vrt_test_flags(void) { return g_test_flags.load(); }
+
+extern "C" int vrt_build_flag(const char *name, int64_t *value)
+{
+        if (!name || !value)
+                return fail(VRT_E_INVALID, "null argument");
+        if (!build_flag(name, value))
+                return fail(VRT_E_INVALID, "unknown build flag %s", name);
+        return VRT_OK;
+}
+
 static void fill_render_params(vrt_scene *s, const vrt_camera *cam,
                                const vrt_film *film, int rank, int nranks,
                                RenderParams *p)
@@ -1256,7 +1277,9 @@ static int queue_take(vrt_scene *s, hipStream_t st, WorkQueue *q, int *slot)
 static int queue_release(vrt_scene *s, int slot, hipStream_t st, const int slice_units[8], int waves)
 {
         for (int x = 0; x < 8; ++x)
-                if (slice_units[x] > 0)
+                if (waves < 0)  // the launch's last wave zeroed the counters (k_render_p)
+                        s->q_base[slot][x] = 0;
+                else if (slice_units[x] > 0)
                         s->q_base[slot][x] += (uint32_t)slice_units[x] + (uint32_t)waves;
         HIPCHK(hipEventRecord(s->q_ev[slot], st));
         s->q_live[slot] = true;
@@ -2036,13 +2059,17 @@ extern "C" int vrt_lightmap_nodes(vrt_scene *s, uint64_t *key, float *coverage, 
                 return VRT_E_NODEVICE;
         if (!s || !key)
                 return fail(VRT_E_INVALID, "null argument");
+        std::lock_guard<std::mutex> lk(s->mu);
         if (s->lm_cur < 0)
                 return fail(VRT_E_INVALID, "no light map: call vrt_lightmap_build first");
-        std::lock_guard<std::mutex> lk(s->mu);
         HIPCHK(hipSetDevice(s->device));
         const size_t n = s->nodes.size();
         std::vector<LMRec> lm(n);
-        HIPCHK(hipDeviceSynchronize());  // the set may be filled on another stream (trace frames)
+        // the set may be filled on the scene stream and read on callers'
+        // streams (trace frames): its last user's event covers both
+        HIPCHK(hipStreamSynchronize(s->stream));
+        if (s->ts[s->lm_cur].live)
+                HIPCHK(hipEventSynchronize(s->ts[s->lm_cur].ev));
         HIPCHK(hipMemcpy(lm.data(), s->ts[s->lm_cur].lm, n * sizeof(LMRec), hipMemcpyDeviceToHost));
         for (size_t l = 0; l + 1 < s->level_begin.size(); ++l)
                 for (int64_t i = s->level_begin[l]; i < s->level_begin[l + 1]; ++i) {
@@ -2185,8 +2212,6 @@ extern "C" int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam, cons
                 return fail(VRT_E_INVALID, "null argument");
         if (int rc = film_ok(film))
                 return rc;
-        if (s->lm_cur < 0)
-                return fail(VRT_E_INVALID, "no light map: call vrt_lightmap_build first");
         if (nranks < 1 || rank < 0 || rank >= nranks)
                 return fail(VRT_E_INVALID, "rank %d of %d", rank, nranks);
         if (image_layout && nranks != 1)
@@ -2194,6 +2219,8 @@ extern "C" int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam, cons
         if (int rc = trace_ok(s, min_voxel))
                 return rc;
         std::lock_guard<std::mutex> lk(s->mu);
+        if (s->lm_cur < 0)
+                return fail(VRT_E_INVALID, "no light map: call vrt_lightmap_build first");
         HIPCHK(hipSetDevice(s->device));
         const int set = s->lm_cur;  // the latest light map
         TraceParams tp0, tp;
@@ -2267,10 +2294,20 @@ extern "C" int vrt_trace_frame_device(vrt_scene *s, const vrt_camera *light_cam,
                 HIPCHK(launch_trace_prim(tp, st));
                 return VRT_OK;
         };
-        if (int rc = lightmap_enqueue(s, set, light_cam, light_film, &nhit, overlap, s->lm_ev))
+        if (int rc = lightmap_enqueue(s, set, light_cam, light_film, &nhit, overlap, s->lm_ev)) {
+                // whatever was enqueued on either stream (the light pass on
+                // the scene's, the primary march on the caller's) finishes
+                // before the set's next user starts
+                if (hipEventRecord(s->lm_ev, s->stream) == hipSuccess)
+                        (void)hipStreamWaitEvent(st, s->lm_ev, 0);
+                (void)ts_release(s, set, st);
                 return rc;
+        }
         HIPCHK(hipStreamWaitEvent(st, s->lm_ev, 0));
-        HIPCHK(launch_cones(tp, st));
+        if (hipError_t e = launch_cones(tp, st)) {
+                (void)ts_release(s, set, st);
+                return fail(VRT_E_DEVICE, "cone pass launch failed: %s", hipGetErrorString(e));
+        }
         if (int rc = ts_release(s, set, st))
                 return rc;
         if (hits)
@@ -2287,11 +2324,11 @@ extern "C" int vrt_render_trace(vrt_scene *s, const vrt_camera *cam, const vrt_f
                 return fail(VRT_E_INVALID, "null argument");
         if (int rc = film_ok(film))
                 return rc;
-        if (s->lm_cur < 0)
-                return fail(VRT_E_INVALID, "no light map: call vrt_lightmap_build first");
         if (int rc = trace_ok(s, min_voxel))
                 return rc;
         std::lock_guard<std::mutex> lk(s->mu);
+        if (s->lm_cur < 0)
+                return fail(VRT_E_INVALID, "no light map: call vrt_lightmap_build first");
         HIPCHK(hipSetDevice(s->device));
         const int set = s->lm_cur;
         const size_t npix = (size_t)film->nx * film->ny, ns = npix * 4;

@@ -531,6 +531,9 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,
                             const SpillQueues *sq = nullptr);
 // the compaction settings of this build (VRT_SEC_SPILL*), cap left 0
 SpillQueues spill_defaults();
+// a path-selecting compile-time switch of the kernel build by name (false:
+// unknown name) -- vrt_build_flag
+bool build_flag(const char *name, int64_t *value);
 hipError_t launch_light(const LightParams &p, hipStream_t st);
 hipError_t light_diag_copy(void *host, size_t bytes);  // VRT_LIGHT_DIAG builds
 // samp: n x 6 floats followed by room for their sorted copy (n x 6);

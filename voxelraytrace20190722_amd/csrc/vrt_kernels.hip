@@ -2071,6 +2071,21 @@ constexpr int kCollectiveReserve = 32;
 #ifndef VRT_LDS_NODES
 #define VRT_LDS_NODES 0
 #endif
+// 1: a wave reads another slice's counter before adding to it and skips a
+// drained slice, so a wave makes one failing add (its own slice) instead of
+// eight; the adds are then no longer a fixed count, so the launch's last wave
+// (kRenderDoneWord) zeroes the counters and the host resets the slot's bases
+// (queue_release with waves < 0)
+#ifndef VRT_Q_PRECHECK
+#define VRT_Q_PRECHECK 0
+#endif
+// 1: a wave whose own slice is drained (the launch's tail: it helps the other
+// XCDs' slices) raises its issue priority, so with frames in flight the tail
+// of frame k runs ahead of frame k+1's bulk waves on the same SIMDs
+#ifndef VRT_TAIL_PRIO
+#define VRT_TAIL_PRIO 0
+#endif
+constexpr int kRenderDoneWord = kDeferDoneWord + 16;  // in WorkQueue::defer (the deferred pass's line)
 template <bool kFastOnly>
 __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_render_p(RenderParams p)
 {
@@ -2084,6 +2099,14 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
                 const int units = p.tiles_this_rank * 4, n = slice_size(units, x, VRT_SLICE_CHUNK);
                 if (n <= 0)
                         continue;
+                if (VRT_TAIL_PRIO && j == 1)
+                        __builtin_amdgcn_s_setprio(2);
+                if (VRT_Q_PRECHECK && j > 0) {
+                        const uint32_t c = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                p.q.ctr + x * kQueueStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        if (c - p.q.base[x] >= (uint32_t)n)
+                                continue;
+                }
                 for (;;) {
                         const uint32_t u = take_unit(p.q.ctr + x * kQueueStride) - p.q.base[x];
                         if (u >= (uint32_t)n)
@@ -2126,6 +2149,19 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
                                                 p.q.defer[kDeferList + x * kDeferSliceCap + d] = (uint32_t)kq;
                                 }
                         }
+                }
+        }
+        if (VRT_Q_PRECHECK) {
+                // every counter add of this wave has returned (each take's
+                // value was used) before this add: the last wave to get here
+                // sees no later add and zeroes the counters for the slot's
+                // next launch
+                const uint32_t fin = take_unit(p.q.defer + kRenderDoneWord);
+                if (fin == gridDim.x * (uint32_t)(kPersistBlock / 64) - 1u) {
+#pragma unroll
+                        for (int x = 0; x < 8; ++x)
+                                p.q.ctr[x * kQueueStride] = 0u;
+                        p.q.defer[kRenderDoneWord] = 0u;
                 }
         }
 }
@@ -3521,8 +3557,9 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 }
                 // failing adds per slice counter: every wave visits every
                 // slice (VRT_PERSIST_HELP), or only its own XCD's (g is a
-                // multiple of 8: g/8 blocks per XCD residue)
-                *q_waves = (VRT_PERSIST_HELP ? g : g / 8) * (kPersistBlock / 64);
+                // multiple of 8: g/8 blocks per XCD residue); with
+                // VRT_Q_PRECHECK the launch zeroes its counters itself (-1)
+                *q_waves = VRT_Q_PRECHECK ? -1 : (VRT_PERSIST_HELP ? g : g / 8) * (kPersistBlock / 64);
                 for (int x = 0; x < 8; ++x)
                         slice_units[x] = slice_size(p.tiles_this_rank * 4, x, VRT_SLICE_CHUNK);
                 return hipGetLastError();
@@ -4680,6 +4717,37 @@ hipError_t launch_lm_aux(const NodeRec *nodes, const LMRec *lm, int64_t n, float
                 return hipSuccess;
         hipLaunchKernelGGL(k_lm_aux, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nodes, lm, n, cc, bad);
         return hipGetLastError();
+}
+
+// The compile-time switches of this kernel build that select a path
+// (vrt_build_flag): the tests assert on them, so a build that silently turns
+// a path off (e.g. config 5's compaction, VRT_SEC_SPILL_T=0) fails its tests.
+bool build_flag(const char *name, int64_t *value)
+{
+        static const struct {
+                const char *name;
+                int64_t value;
+        } kFlags[] = {
+                { "VRT_SEC_SPILL_T", VRT_SEC_SPILL_T },
+                { "VRT_SEC_STREAM", VRT_SEC_STREAM },
+                { "VRT_SEC_ANY", VRT_SEC_ANY },
+                { "VRT_SEC_PERSIST", VRT_SEC_PERSIST },
+                { "VRT_SEC_SLICE_CHUNK", VRT_SEC_SLICE_CHUNK },
+                { "VRT_PERSIST", VRT_PERSIST },
+                { "VRT_PERSIST_FAST", VRT_PERSIST_FAST },
+                { "VRT_SLICE_CHUNK", VRT_SLICE_CHUNK },
+                { "VRT_NODE_BOX", VRT_NODE_BOX },
+                { "VRT_DEAL_BLOCK", VRT_DEAL_BLOCK },
+                { "VRT_DEAL_WEIGHT", VRT_DEAL_WEIGHT },
+                { "VRT_LIGHT_BUDGET", VRT_LIGHT_BUDGET },
+                { "VRT_PRIM_BUDGET", VRT_PRIM_BUDGET },
+        };
+        for (const auto &f : kFlags)
+                if (std::strcmp(f.name, name) == 0) {
+                        *value = f.value;
+                        return true;
+                }
+        return false;
 }
 
 }  // namespace vrt
