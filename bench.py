@@ -40,6 +40,12 @@ VALU_WAVE_INSTR_PER_CYCLE = N_CU * 4 / 2
 MAX_CLOCK_GHZ = 2.4     # MI355X max engine clock (MI355X_MICROARCH.md chip table)
 
 
+CPU_NOTE = ("kind 'port': oracle/vrt_oracle.c, the C restatement of the reference path, scheduled as render_mt "
+            "(64 tile tasks over hardware_concurrency threads); the reference's own thread_pool_cpp path cannot "
+            "be built here without stand-ins for headers libstdc++ 11 lacks (SURVEY §8(c), DESIGN §2), so no "
+            "calibration ratio to it exists (BASELINE.md)")
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -863,6 +869,11 @@ def main():
         else:
             per_rank = [{"rank": 0, "share_of_rank": cur["share"],
                          **{k_: round(v_, 4) for k_, v_ in zip(RANK_FIELDS, vals)}}]
+    # the scene's device memory after the timed frames: octree + triangles +
+    # textures, and the scratch it keeps between calls (config 5's
+    # compaction queues among it)
+    scr, spl = tree.scratch_bytes()
+    dev_bytes = {"scene": int(info.device_bytes), "scratch": int(scr), "compaction_scratch": int(spl)}
     # per-frame device time: the launch span with one frame in flight; with
     # several, spans overlap (a span also holds the wait for the CUs the
     # previous frame still occupies), so the frame time is the step time
@@ -1041,7 +1052,7 @@ def main():
                          1.0, 1.0, hw, hh, res, nthreads=nth, samples=False)
         t2_ = time.perf_counter()
         tr = (t2_ - t1_) * (a.width * a.height) / (hw * hh)
-        cpu = {"value": round(1.0 / ((t1_ - t0_) + tr), 5), "unit": "frames/s", "cores": eff_cores(nth, ci), "threads": nth, "kind": "port",
+        cpu = {"value": round(1.0 / ((t1_ - t0_) + tr), 5), "unit": "frames/s", "cores": eff_cores(nth, ci), "threads": nth, "kind": "port", "note": CPU_NOTE,
                "nproc": ci["nproc"], "cgroup_quota_cpus": ci["cgroup_quota_cpus"], "cpu_model": ci["model"],
                "sample": f"light map {a.light_n}^2 x4 + filter ({t1_ - t0_:.1f} s) + cone-traced {hw}x{hh} x4 "
                          f"({t2_ - t1_:.1f} s, scaled x{(a.width * a.height) / (hw * hh):.0f} to "
@@ -1084,7 +1095,7 @@ def main():
                 raise SystemExit(f"pose {pi}: oracle traced {nr} rays, the GPU count is {frame_rays[pi]}")
             frames += 1
         med = float(np.median(times))
-        cpu = {"value": round(float(np.median(rates)) / 1e6, 4), "unit": "Mrays/s", "cores": eff_cores(nth, ci), "threads": nth, "kind": "port",
+        cpu = {"value": round(float(np.median(rates)) / 1e6, 4), "unit": "Mrays/s", "cores": eff_cores(nth, ci), "threads": nth, "kind": "port", "note": CPU_NOTE,
                "nproc": ci["nproc"], "affinity_cpus": ci["affinity"], "cgroup_quota_cpus": ci["cgroup_quota_cpus"],
                "cpu_model": ci["model"],
                "frame_s": {"warmup": round(warm_s, 3), "median": round(med, 3), "min": round(min(times), 3),
@@ -1127,7 +1138,7 @@ def main():
             checked += 1
             frames += 1
         med = float(np.median(times))
-        cpu = {"value": round(rays_per_frame / med / 1e6, 4), "unit": "Mrays/s", "cores": eff_cores(nth, ci), "threads": nth, "kind": "port",
+        cpu = {"value": round(rays_per_frame / med / 1e6, 4), "unit": "Mrays/s", "cores": eff_cores(nth, ci), "threads": nth, "kind": "port", "note": CPU_NOTE,
                "nproc": ci["nproc"], "affinity_cpus": ci["affinity"], "cgroup_quota_cpus": ci["cgroup_quota_cpus"],
                "cpu_model": ci["model"],
                "frame_s": {"warmup": round(warm_s, 3), "median": round(med, 3), "min": round(min(times), 3),
@@ -1169,6 +1180,7 @@ def main():
                 "roofline": roof,
                 "roofline_per_kernel": trace_kernels,
                 "cpu_baseline": cpu,
+                "device_bytes": dev_bytes,
             }
             print(json.dumps(out), flush=True)
             if world > 1:
@@ -1212,6 +1224,7 @@ def main():
         }
         if secondary and trace_kernels:
             out["roofline_per_kernel"] = trace_kernels
+        out["device_bytes"] = dev_bytes
         if per_rank:
             out["per_rank"] = per_rank
         if d9:

@@ -291,6 +291,12 @@ int vrt_test_flags(void);
  * used) by the scene's last config-5 launch; waits for it.  All 0 when that
  * launch used no compaction. */
 int vrt_secondary_spill_counts(vrt_scene *s, int64_t counts[4]);
+/* Device bytes the scene holds beyond its octree, triangles and textures
+ * (vrt_scene_info().device_bytes): per-call scratch kept between calls --
+ * config 5's compaction queues (*spill_bytes, may be NULL), the light-map
+ * build's scratch and light-map sets, the trace records, the host-output
+ * image. */
+int vrt_scene_scratch_bytes(vrt_scene *s, int64_t *bytes, int64_t *spill_bytes);
 
 /* The kernels' own travorder sort (std::sort of the 8 Items by dist,
  * VRT/voxel_octree.cc:77-97) and ray_march_isect min_element

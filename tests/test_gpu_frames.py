@@ -137,6 +137,10 @@ def test_c5_1080p_depth8_secondary_whole_frame(proxy):
     tree.render_secondary_device(cam, film, 64, 0, 1, prim.data_ptr(), dvis.data_ptr(), None)
     torch.cuda.synchronize()
     assert np.array_equal(bits(dvis.cpu().numpy()), bits(ovis))
+    # the compaction scratch is sized from the queue's use, not for every ray
+    # (DESIGN §4.3): at most 1 GiB for a 1080p frame, one set for calls that
+    # do not overlap
+    assert tree.scratch_bytes()[1] <= 1 << 30, tree.scratch_bytes()
 
 
 def test_two_streams_share_one_scene(proxy):

@@ -430,6 +430,13 @@ class VoxelOctree:
         check(lib().vrt_secondary_spill_counts(self.h, c), "vrt_secondary_spill_counts")
         return list(c)
 
+    def scratch_bytes(self):
+        """(total, compaction) device bytes of scratch the scene keeps between
+        calls (vrt_scene_scratch_bytes)."""
+        t, sp = C.c_int64(), C.c_int64()
+        check(lib().vrt_scene_scratch_bytes(self.h, C.byref(t), C.byref(sp)), "vrt_scene_scratch_bytes")
+        return t.value, sp.value
+
     def last_kernel_ms(self):
         ms = C.c_float()
         check(lib().vrt_last_kernel_ms(self.h, C.byref(ms)), "vrt_last_kernel_ms")

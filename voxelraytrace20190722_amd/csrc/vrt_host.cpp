@@ -372,6 +372,9 @@ struct vrt_scene {
         uint32_t spill_cap[2] = {};  // chunks per queue
         hipEvent_t spill_ev[2] = {};
         bool spill_live[2] = {};
+        hipStream_t spill_stream[2] = {};  // the set's last user (a stream keeps its set)
+        uint32_t *h_spill = nullptr;       // pinned: per set, chunks phase A took in its last launch
+        uint32_t spill_want = 0;           // queue-0 chunks the next launch sizes for (0: first estimate)
         int spill_next = 0;
         int spill_last = -1;  // the set the last config-5 launch compacted with (vrt_secondary_spill_counts)
         // device
@@ -384,6 +387,10 @@ struct vrt_scene {
         // of kQueueSlots counter sets, each with its bases and the event of
         // its last launch
         uint32_t *d_queue = nullptr;
+        // budgeted render (render_uses_tail): per queue slot, the list of
+        // pixels left to k_render_tail (rtail_words words each)
+        uint32_t *d_rtail = nullptr;
+        size_t rtail_words = 0;
         uint32_t q_base[kQueueSlots][8] = {};
         hipEvent_t q_ev[kQueueSlots] = {};
         bool q_live[kQueueSlots] = {};
@@ -1040,6 +1047,8 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                                 (void)hipEventSynchronize(s->spill_ev[k]);
                 if (s->d_mem)
                         (void)hipFree(s->d_mem);
+                if (s->d_rtail)
+                        (void)hipFree(s->d_rtail);
                 for (TraceSet &t : s->ts) {
                         if (t.lm)
                                 (void)hipFree(t.lm);
@@ -1050,6 +1059,8 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                 }
                 if (s->d_light)
                         (void)hipFree(s->d_light);
+                if (s->h_spill)
+                        (void)hipHostFree(s->h_spill);
                 for (int k = 0; k < 2; ++k) {
                         if (s->d_spill[k])
                                 (void)hipFree(s->d_spill[k]);
@@ -1294,9 +1305,34 @@ static int queue_release(vrt_scene *s, int slot, hipStream_t st, const int slice
 static void queue_reset(vrt_scene *s, int slot, hipStream_t st)
 {
         (void)hipMemsetAsync(s->d_queue + (size_t)slot * kQueueWords, 0, kQueueBytes, st);
+        if (s->d_rtail)  // the budgeted render's list count and done word
+                (void)hipMemsetAsync(s->d_rtail + (size_t)slot * s->rtail_words, 0, kRenderTailList * 4, st);
         std::memset(s->q_base[slot], 0, sizeof s->q_base[slot]);
         if (hipEventRecord(s->q_ev[slot], st) == hipSuccess)
                 s->q_live[slot] = true;
+}
+
+// The budgeted render's left-pixel list of queue slot `slot`, grown to this
+// launch's pixels (budget builds only; caller holds s->mu).
+static int rtail_setup(vrt_scene *s, RenderParams &p, int slot)
+{
+        p.rtail = nullptr;
+        if (!render_budget_built() || slot < 0)
+                return VRT_OK;
+        const size_t words = kRenderTailList + (size_t)p.tiles_this_rank * 64;
+        if (s->rtail_words < words) {
+                if (s->d_rtail) {
+                        HIPCHK(hipDeviceSynchronize());  // launches on any stream may use the lists
+                        (void)hipFree(s->d_rtail);
+                        s->d_rtail = nullptr;
+                        s->rtail_words = 0;
+                }
+                HIPCHK(hipMalloc(&s->d_rtail, words * 4 * kQueueSlots));
+                HIPCHK(hipMemset(s->d_rtail, 0, words * 4 * kQueueSlots));
+                s->rtail_words = words;
+        }
+        p.rtail = s->d_rtail + (size_t)slot * s->rtail_words;
+        return VRT_OK;
 }
 
 // One render launch on stream st (caller holds s->mu).
@@ -1306,6 +1342,8 @@ static int render_launch(vrt_scene *s, RenderParams &p, bool instrumented, hipSt
         (void)hipGetLastError();  // a leftover error of an earlier call is not this launch's
         if (render_kind(p, instrumented) != kRenderGrid) {
                 if (int rc = queue_take(s, st, &p.q, &slot))
+                        return rc;
+                if (int rc = rtail_setup(s, p, slot))
                         return rc;
         }
         int waves = 0, units[8];
@@ -1323,32 +1361,64 @@ static int render_launch(vrt_scene *s, RenderParams &p, bool instrumented, hipSt
 static int ts_acquire(vrt_scene *s, int i, hipStream_t st);
 static int ts_release(vrt_scene *s, int i, hipStream_t st);
 
-// Compaction queues of one config-5 launch (SpillQueues): room
-// for every secondary ray of this rank, in chunks, up to kSpillCapMax records
-// per queue (a full queue only means the rays beyond it finish in their
-// first wave); the round counters zeroed on the stream.  The scene keeps two
-// sets, taken by alternate launches (two frames in flight on two streams);
-// a set's next user waits for the event of its last.  sq->nchunks stays 0
-// (no compaction) when the build disables it or the allocation fails.
-constexpr uint32_t kSpillCapMax = 1u << 24;  // 2 GiB of records per queue
+// Compaction queue of one config-5 launch (SpillQueues).  Its
+// size is an estimate: a full queue only means the rays beyond it finish in
+// their first wave (spill_reserve returns no threshold), so any size gives
+// the same images.  The first launch sizes queue 0 for 1/32 of the rank's
+// secondary rays (1080p: 4.1 M records, 0.5 GiB); after every launch the
+// chunks phase A took are copied to pinned memory, and a later launch sizes
+// for 1.5 x that (x 2 after an overflow), growing, never shrinking.  Only
+// queue 0's records are allocated: the one pooled resume round walks every
+// saved ray to its end (queue 1's fill words list the streaming round's
+// leftover chunks).  The scene keeps two sets; a stream keeps using the set
+// it used last (stream order protects it), a new stream takes the other one
+// (frames in flight on two streams), waiting for its last user's event.
+// sq->nchunks stays 0 (no compaction) when the build disables it or the
+// allocation fails.
+constexpr uint32_t kSpillCapMax = 1u << 24;  // chunks: 2 GiB of records at most
 static int spill_setup(vrt_scene *s, int64_t rays, hipStream_t st, SpillQueues *sq, int *set)
 {
         *sq = spill_defaults();
         *set = -1;
         if (sq->t_first == 0 || rays <= 0)
                 return VRT_OK;
-        // the next of the two sets; this stream first waits for its last user
-        const int k = s->spill_next;
-        s->spill_next ^= 1;
+        // this stream's own set; else an allocated set whose last launch has
+        // finished (a second set is allocated only for frames in flight on
+        // two streams); else the next one
+        int k = -1;
+        for (int i = 0; i < 2 && k < 0; ++i)
+                if (s->spill_live[i] && s->spill_stream[i] == st)
+                        k = i;
+        for (int i = 0; i < 2 && k < 0; ++i)
+                if (s->d_spill[i] && (!s->spill_live[i] || hipEventQuery(s->spill_ev[i]) == hipSuccess))
+                        k = i;
+        if (k < 0) {
+                k = s->spill_next;
+                s->spill_next ^= 1;
+        }
         if (!s->spill_ev[k])
                 HIPCHK(hipEventCreateWithFlags(&s->spill_ev[k], hipEventDisableTiming));
-        if (s->spill_live[k])
+        if (!s->h_spill) {
+                HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&s->h_spill), 2 * sizeof(uint32_t),
+                                     hipHostMallocDefault));
+                s->h_spill[0] = s->h_spill[1] = 0;
+        }
+        // what the finished launches of either set took
+        for (int i = 0; i < 2; ++i)
+                if (s->spill_live[i] && s->spill_cap[i] && hipEventQuery(s->spill_ev[i]) == hipSuccess) {
+                        const uint32_t took = s->h_spill[i];
+                        const uint64_t w = took >= s->spill_cap[i] ? 2ull * s->spill_cap[i]  // overflowed
+                                                                    : (3ull * took + 1) / 2;
+                        s->spill_want = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(s->spill_want, w), kSpillCapMax);
+                }
+        if (s->spill_live[k] && s->spill_stream[k] != st)
                 HIPCHK(hipStreamWaitEvent(st, s->spill_ev[k], 0));
         // + one partly filled chunk per wave of a resident grid
-        const int64_t want = rays + (int64_t)std::max(1, s->dev.sec_blocks) * 4 * kSpillChunk;
-        const uint32_t nch = (uint32_t)((std::min<int64_t>(want, kSpillCapMax) + kSpillChunk - 1) / kSpillChunk);
+        const int64_t partial = (int64_t)std::max(1, s->dev.sec_blocks) * 4;
+        const int64_t est = s->spill_want ? (int64_t)s->spill_want : (rays / 32 + kSpillChunk - 1) / kSpillChunk;
+        const uint32_t nch = (uint32_t)std::min<int64_t>(std::min<int64_t>(est, (rays + kSpillChunk - 1) / kSpillChunk) +
+                                                                 partial, kSpillCapMax);
         const size_t ctr_bytes = (size_t)kSpillMaxRounds * kSpillCtrStride * 4;
-        const size_t fill_bytes = ((size_t)nch * 4 + 255) & ~(size_t)255;
         if (s->spill_cap[k] < nch) {
                 if (s->d_spill[k]) {
                         HIPCHK(hipDeviceSynchronize());  // earlier launches on any stream may use it
@@ -1356,7 +1426,8 @@ static int spill_setup(vrt_scene *s, int64_t rays, hipStream_t st, SpillQueues *
                         s->d_spill[k] = nullptr;
                         s->spill_cap[k] = 0;
                 }
-                if (hipMalloc(&s->d_spill[k], ctr_bytes + 2 * fill_bytes + 2 * (size_t)nch * kSpillChunk * sizeof(SpillRec)) !=
+                const size_t fb = ((size_t)nch * 4 + 255) & ~(size_t)255;
+                if (hipMalloc(&s->d_spill[k], ctr_bytes + 2 * fb + (size_t)nch * kSpillChunk * sizeof(SpillRec)) !=
                     hipSuccess) {
                         (void)hipGetLastError();
                         s->d_spill[k] = nullptr;
@@ -1370,10 +1441,22 @@ static int spill_setup(vrt_scene *s, int64_t rays, hipStream_t st, SpillQueues *
         sq->fill[0] = reinterpret_cast<uint32_t *>(b + ctr_bytes);
         sq->fill[1] = reinterpret_cast<uint32_t *>(b + ctr_bytes + fb);
         sq->rec[0] = reinterpret_cast<SpillRec *>(b + ctr_bytes + 2 * fb);
-        sq->rec[1] = sq->rec[0] + (size_t)s->spill_cap[k] * kSpillChunk;
+        sq->rec[1] = nullptr;  // the pooled resume round stops no ray
         sq->nchunks = s->spill_cap[k];
         HIPCHK(hipMemsetAsync(sq->ctr, 0, ctr_bytes, st));
         *set = k;
+        return VRT_OK;
+}
+
+// After a config-5 launch with compaction set k on st: its phase-A chunk
+// count to pinned memory (spill_setup reads it once the set's event has
+// passed) and the set's event.
+static int spill_done(vrt_scene *s, int k, const SpillQueues &sq, hipStream_t st)
+{
+        HIPCHK(hipMemcpyAsync(s->h_spill + k, sq.ctr, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(s->spill_ev[k], st));
+        s->spill_live[k] = true;
+        s->spill_stream[k] = st;
         return VRT_OK;
 }
 
@@ -1402,10 +1485,9 @@ static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int ra
         s->spill_last = sq.nchunks > 0 ? set : -1;
         const hipError_t e = launch_secondary(p, spp, rank, nranks, scene_res(s), d_prim, d_vis, s_hit, s_tri,
                                               s_vox, slot >= 0 ? &q : nullptr, st, &waves, units, &sq);
-        if (set >= 0) {
-                HIPCHK(hipEventRecord(s->spill_ev[set], st));
-                s->spill_live[set] = true;
-        }
+        if (set >= 0)
+                if (int rc = spill_done(s, set, sq, st))
+                        return rc;
         if (e != hipSuccess) {
                 if (slot >= 0)
                         queue_reset(s, slot, st);
@@ -1774,6 +1856,30 @@ extern "C" int vrt_render_secondary_device(vrt_scene *s, const vrt_camera *cam,
                 return rc;
         HIPCHK(hipEventRecord(s->ev1, st));
         s->timed = true;
+        return VRT_OK;
+}
+
+extern "C" int vrt_scene_scratch_bytes(vrt_scene *s, int64_t *bytes, int64_t *spill_bytes)
+{
+        if (!s || !bytes)
+                return fail(VRT_E_INVALID, "null argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        int64_t sp = 0;
+        for (int k = 0; k < 2; ++k)
+                if (s->d_spill[k]) {
+                        const int64_t fb = ((int64_t)s->spill_cap[k] * 4 + 255) & ~(int64_t)255;
+                        sp += (int64_t)kSpillMaxRounds * kSpillCtrStride * 4 + 2 * fb +
+                              (int64_t)s->spill_cap[k] * kSpillChunk * (int64_t)sizeof(SpillRec);
+                }
+        int64_t t = sp + (int64_t)s->light_bytes + (int64_t)s->rtail_words * 4 * kQueueSlots + (int64_t)s->ho.bytes;
+        for (const TraceSet &ts : s->ts) {
+                if (ts.lm)
+                        t += (int64_t)s->nodes.size() * (int64_t)(sizeof(LMRec) + sizeof(float4)) + 256;
+                t += (int64_t)ts.rec_bytes;
+        }
+        *bytes = t;
+        if (spill_bytes)
+                *spill_bytes = sp;
         return VRT_OK;
 }
 

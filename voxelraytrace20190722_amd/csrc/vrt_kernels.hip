@@ -1855,7 +1855,8 @@ constexpr int kRenderBlock = 64 * VRT_RENDER_WAVES;
 // standard-range instantiation is compiled in (fewer live registers); a wave
 // whose rays need another path returns false before writing anything and the
 // caller defers the unit to k_render_defer.
-template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kNS = 0>
+template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kNS = 0,
+          int kBudget = 0>
 __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wave, int lane, uint2 *stk,
                                             uint32_t *stk_aux, uint32_t *path_rem)
 {
@@ -1914,7 +1915,7 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         if (kFastOnly) {
                 if (!wave_fast_std(p.sc, r) || (p.test_flags & VRT_TEST_FORCE_DEFER))
                         return false;
-                ray_march<false, true, kS, kFastStd, true, kR64, kNS>(p.sc, r, stk, nullptr, nullptr, m);
+                ray_march<false, true, kS, kFastStd, true, kR64, kNS, kBudget>(p.sc, r, stk, nullptr, nullptr, m);
         } else {
                 ray_march_dispatch<kCount, kS, true, kR64, kNS>(p.sc, r, stk, stk_aux, path_rem, m);
         }
@@ -1938,8 +1939,17 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                         dn = d2;
         }
 
+        // kBudget: a pixel with a sample whose walk hit the budget is left to
+        // k_render_tail (all 4 samples re-walked there, 8 lanes per ray)
+        bool pdef = false;
+        if (kBudget) {
+                const uint64_t dm = __ballot(m.deferred);
+                pdef = dm != 0 && ((dm >> (lane_now() & ~3)) & 0xFull) != 0;
+        }
         f3 col;
-        if (m.hit) {
+        if (pdef) {
+                col = mk3(0.f, 0.f, 0.f);
+        } else if (m.hit) {
                 f3 nrm;
                 RayK rs;  // shade_hit reads the direction only
                 rs.d = dn;
@@ -1979,7 +1989,10 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                 for (int q = 0; q < 3; ++q)  // lane l0 + j's value (a wave64 permute by our own lane id)
                         acc[q] += __int_as_float(__builtin_amdgcn_ds_bpermute((l0 + j) << 2, __float_as_int(cv[q])));
         }
-        if (s == 0) {
+        if (kBudget && s == 0 && pdef) {
+                const uint32_t j = atomicAdd(p.rtail, 1u);  // the deferring lanes' adds: one atomic per wave
+                p.rtail[kRenderTailList + j] = (uint32_t)(k * 4 + wave) << 4 | (uint32_t)(lane >> 2);
+        } else if (s == 0) {
                 float *o;
                 if (p.image_layout)
                         o = p.out + ((size_t)py * c.nx + px) * 3;
@@ -2086,7 +2099,7 @@ constexpr int kCollectiveReserve = 32;
 #define VRT_TAIL_PRIO 0
 #endif
 constexpr int kRenderDoneWord = kDeferDoneWord + 16;  // in WorkQueue::defer (the deferred pass's line)
-template <bool kFastOnly>
+template <bool kFastOnly, int kBudget = 0>
 __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_render_p(RenderParams p)
 {
         constexpr int kNS = kFastOnly ? VRT_LDS_NODES : 0;
@@ -2118,7 +2131,7 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
 #if VRT_UNIT_DIAG
                         const uint32_t dg_u0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kNS>(
+                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kNS, kBudget>(
                                 p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr);
 #if VRT_UNIT_DIAG
                         {
@@ -2216,6 +2229,77 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
                         p.q.defer[x * kQueueStride + kDeferTake] = 0u;
                 }
                 p.q.defer[kDeferDoneWord] = 0u;
+        }
+}
+
+// The pixels k_render_p<true, kBudget> left (a sample's walk reached the
+// triangle-test budget): each of a pixel's 4 gen_rays4 samples re-walked
+// from the root by a group of 8 lanes on that one ray (leaf_isect_grp: the
+// leaf's records split over the group, ray_march_isect's first minimum
+// kept), 2 pixels per wave; shading, and Film::add of the 4 samples in order
+// -- the values the unbudgeted walk writes.  The last wave zeroes the list's
+// count for the queue slot's next launch.
+template <bool kR64>
+__global__ __launch_bounds__(64) void k_render_tail(RenderParams p)
+{
+        constexpr int kG = 8;
+        __shared__ uint2 stk[kStack * 64];
+        const uint32_t n = __builtin_amdgcn_readfirstlane(p.rtail[0]);
+        const int lane = threadIdx.x, half = lane >> 5, s = (lane >> 3) & 3;
+        const CamParams &c = p.cam;
+        for (uint32_t i0 = blockIdx.x * 2; i0 < n; i0 += gridDim.x * 2) {
+                const uint32_t i = i0 + (uint32_t)half;
+                int px = 0, py = 0, k = 0, lx = 0, ly = 0;
+                f3 cq = mk3(0.f, 0.f, 0.f);
+                if (i < n) {  // whole groups: both halves' lanes alike
+                        const uint32_t e = p.rtail[kRenderTailList + i];
+                        const int kq = (int)(e >> 4), pix = (int)(e & 15u), wave = kq & 3;
+                        k = kq >> 2;
+                        int tx, ty;
+                        deal_tile(tile_deal(p.ntx, p.nty, p.nranks), p.rank, k, tx, ty);
+                        lx = (wave & 1) * 4 + (pix & 3);
+                        ly = (wave >> 1) * 4 + (pix >> 2);
+                        px = tx * 8 + lx;
+                        py = (ty + p.ty0) * 8 + ly;
+                        const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py, sample_x(s),
+                                                 sample_y(s));
+                        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]), dn, c.tmin, c.tmax);
+                        MarchResult m;
+                        ray_march_dispatch<false, 64, kG, kR64>(p.sc, r, stk + lane, nullptr, nullptr, m);
+                        f3 col;
+                        if (m.hit) {
+                                f3 nrm;
+                                col = shade_hit(p.sc, r, m, nrm);
+                        } else {
+                                col = sky(dn.y);
+                        }
+                        cq = col * .25f;
+                }
+                // Film::add of samples 0..3 (lanes half*32 + 8j) in order, from zero
+                const int l0 = lane & 32;
+                float acc[3] = { 0.0f, 0.0f, 0.0f };
+                const float cv[3] = { cq.x, cq.y, cq.z };
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                        for (int q = 0; q < 3; ++q)
+                                acc[q] += __int_as_float(
+                                        __builtin_amdgcn_ds_bpermute((l0 + 8 * j) << 2, __float_as_int(cv[q])));
+                }
+                if (i < n && (lane & 31) == 0) {
+                        float *o = p.image_layout ? p.out + ((size_t)py * c.nx + px) * 3
+                                                  : p.out + ((size_t)k * 64 + ly * 8 + lx) * 3;
+                        o[0] = acc[0];
+                        o[1] = acc[1];
+                        o[2] = acc[2];
+                }
+        }
+        // every wave has read the count: the last one zeroes it (and the done
+        // word) for the slot's next launch
+        const uint32_t fin = take_unit(p.rtail + kRenderTailDone);
+        if (fin == gridDim.x - 1u) {
+                p.rtail[0] = 0u;
+                p.rtail[kRenderTailDone] = 0u;
         }
 }
 
@@ -3310,6 +3394,28 @@ hipError_t launch_selftest_order(const float *dist, const uint32_t *hm, int64_t 
         return hipGetLastError();
 }
 
+// Budgeted primary walks (k_render_p<true, kBudget> + k_render_tail): a
+// walk that would pass VRT_RENDER_BUDGET triangle tests stops and its pixel
+// is re-rendered by k_render_tail with 8 lanes per ray, so a unit of long
+// rays no longer holds one wave for its whole walk.  0 = off; by default only
+// for the shares of a multi-rank frame (VRT_RENDER_BUDGET_MULTI_ONLY), whose
+// frames are short enough that one such unit sets the frame's end.
+#ifndef VRT_RENDER_BUDGET
+#define VRT_RENDER_BUDGET 0
+#endif
+#ifndef VRT_RENDER_BUDGET_MULTI_ONLY
+#define VRT_RENDER_BUDGET_MULTI_ONLY 1
+#endif
+#ifndef VRT_RENDER_TAIL_GRID
+#define VRT_RENDER_TAIL_GRID 1024
+#endif
+bool render_uses_tail(const RenderParams &p)
+{
+        return VRT_RENDER_BUDGET > 0 && p.rtail && (!VRT_RENDER_BUDGET_MULTI_ONLY || p.nranks > 1) &&
+               render_kind(p, false) == kRenderPersistFast;
+}
+bool render_budget_built() { return VRT_RENDER_BUDGET > 0; }
+
 #ifndef VRT_PERSIST
 #define VRT_PERSIST 1
 #endif
@@ -3478,6 +3584,15 @@ hipError_t persistent_blocks(int *render_blocks, int *sec_blocks)
         if (e != hipSuccess)
                 return e;
         *render_blocks = std::min(a, b);
+#if VRT_RENDER_BUDGET > 0
+        {
+                const int c = resident_blocks(reinterpret_cast<const void *>(k_render_p<true, VRT_RENDER_BUDGET>),
+                                              kPersistBlock, prop, &e);
+                if (e != hipSuccess)
+                        return e;
+                *render_blocks = std::min(*render_blocks, c);
+        }
+#endif
         int sb = 1 << 30;
         const void *sk[4] = { reinterpret_cast<const void *>(k_secondary_p<false, false>),
                               reinterpret_cast<const void *>(k_secondary_p<false, true>),
@@ -3510,9 +3625,19 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 const int cap = std::max(8, p.nranks > 1 ? full - kCollectiveReserve : full);
                 const int g = std::min(cap, need);
                 if (kind == kRenderPersistFast) {
-                        hipLaunchKernelGGL(k_render_p<true>, dim3(g), dim3(kPersistBlock), 0, st, p);
+                        const bool tail = render_uses_tail(p);
+                        void (*kern)(RenderParams) = k_render_p<true>;
+#if VRT_RENDER_BUDGET > 0
+                        if (tail)
+                                kern = k_render_p<true, VRT_RENDER_BUDGET>;
+#endif
+                        hipLaunchKernelGGL(kern, dim3(g), dim3(kPersistBlock), 0, st, p);
                         if (hipError_t e = hipGetLastError())
                                 return e;
+#if VRT_RENDER_BUDGET > 0
+                        if (tail)
+                                hipLaunchKernelGGL(k_render_tail<false>, dim3(VRT_RENDER_TAIL_GRID), dim3(64), 0, st, p);
+#endif
 #if VRT_UNIT_DIAG
                         {
                                 static int ndump = 0;
@@ -4741,6 +4866,7 @@ bool build_flag(const char *name, int64_t *value)
                 { "VRT_DEAL_WEIGHT", VRT_DEAL_WEIGHT },
                 { "VRT_LIGHT_BUDGET", VRT_LIGHT_BUDGET },
                 { "VRT_PRIM_BUDGET", VRT_PRIM_BUDGET },
+                { "VRT_RENDER_BUDGET", VRT_RENDER_BUDGET },
         };
         for (const auto &f : kFlags)
                 if (std::strcmp(f.name, name) == 0) {
