@@ -281,6 +281,10 @@ int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
 /* VRT_TEST_PRIM_TAIL does the same for the primary pass of the cone-traced
  * render (vrt_render_trace*, vrt_trace_frame_device). */
 #define VRT_TEST_PRIM_TAIL 64
+/* VRT_TEST_NO_STREAM makes config 5's resume round walk queue 0 chunk by
+ * chunk (k_sec_resume) instead of streaming it -- the path of films of 2^26
+ * pixels or more. */
+#define VRT_TEST_NO_STREAM 128
 #define VRT_TEST_VIRTUAL_RANKS_N(n) (VRT_TEST_VIRTUAL_RANKS | ((n) << 8))
 int vrt_set_test_flags(int flags);
 /* The current vrt_set_test_flags value (so a caller can restore it). */

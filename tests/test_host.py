@@ -331,8 +331,7 @@ def test_kernel_build_flags_are_the_defaults():
     fast-only primary render); unknown names are rejected."""
     assert vrt.build_flag("VRT_SEC_SPILL_T") > 0
     assert vrt.build_flag("VRT_SEC_STREAM") == 1
-    assert vrt.build_flag("VRT_PERSIST") == 1 and vrt.build_flag("VRT_PERSIST_FAST") == 1
-    assert vrt.build_flag("VRT_NODE_BOX") == 1
+    assert vrt.build_flag("VRT_SLICE_CHUNK") > 0
     with pytest.raises(vrt.VrtError):
         vrt.build_flag("VRT_NO_SUCH_FLAG")
 

@@ -688,9 +688,9 @@ extern "C" int vrt_device_count(int *n)
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// DevScene::mnodes: the nodes with every non-root leaf that holds triangles
-// carrying the union box of its triangles, enlarged by eps = 2^-16 * the
-// root's largest extent and rounded outward to float.  Sets lb_center and
+// DevScene::xnodes: every node's own record followed by the union box of all
+// triangles below it (a leaf: its own), enlarged by eps = 2^-16 * the root's
+// largest extent and rounded outward to float.  Sets lb_center and
 // lb_reach = 16 * that extent: for a ray origin within lb_reach of the
 // centre (per axis) and a point of a leaf's triangles, every slab distance
 // |p - o| / |d| is below 17 * extent / |d|, the three fp32 roundings of
@@ -698,20 +698,13 @@ static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 // eps / |d|, so the fp32 line test on the enlarged box passes whenever the
 // exact line meets the unenlarged one -- and intersect_triangle3 accepts a
 // triangle only where the line meets it (up to its fp64 rounding, far below
-// eps).  VRT_LEAF_BOX=0: mnodes = nodes.
-#ifndef VRT_LEAF_BOX
-#define VRT_LEAF_BOX 1
-#endif
-//
-// DevScene::xnodes (VRT_NODE_BOX): every node's own record followed by the
-// union box of all triangles below it (a leaf: its own), enlarged the same
-// way -- the same bound holds, as every such triangle lies in the root box.
-// Nodes with no triangle below them (never visited by the content-masked
-// walk) and every node when the skip is off carry their voxel box.
-static std::vector<NodeRec> march_nodes(vrt_scene *s, const vrt_scene_desc *d, std::vector<XNodeRec> &xn)
+// eps); an internal node's box bounds the triangles of its leaves, which all
+// lie in the root box, so the same bound holds.  Nodes with no triangle below
+// them (never visited by the content-masked walk), and every node of a scene
+// whose extent is not finite and positive (no skip), carry their voxel box.
+static void march_nodes(vrt_scene *s, const vrt_scene_desc *d, std::vector<XNodeRec> &xn)
 {
-        std::vector<NodeRec> mn = s->nodes;
-        const size_t nn = mn.size();
+        const size_t nn = s->nodes.size();
         xn.resize(nn);
         for (size_t i = 0; i < nn; ++i) {
                 xn[i] = XNodeRec{};
@@ -727,9 +720,9 @@ static std::vector<NodeRec> march_nodes(vrt_scene *s, const vrt_scene_desc *d, s
                 s->dev.lb_center[k] = 0.5f * (s->info.root_min[k] + s->info.root_max[k]);
         }
         s->dev.lb_reach = 16.f * ext;
-        if (!VRT_LEAF_BOX || !(ext > 0.f) || !std::isfinite(ext)) {
+        if (!(ext > 0.f) || !std::isfinite(ext)) {
                 s->dev.lb_reach = -1.f;  // never skip
-                return mn;
+                return;
         }
         const double eps = std::ldexp((double)ext, -16);
         // unenlarged triangle boxes, bottom-up (children follow their parent
@@ -774,13 +767,7 @@ static std::vector<NodeRec> march_nodes(vrt_scene *s, const vrt_scene_desc *d, s
                         xn[i].tmin[k] = bl[k];
                         xn[i].tmax[k] = bh[k];
                 }
-                if (mn[i].a & kLeafBit)
-                        for (int k = 0; k < 3; ++k) {
-                                mn[i].bmin[k] = bl[k];
-                                mn[i].bmax[k] = bh[k];
-                        }
         }
-        return mn;
 }
 
 static int upload(vrt_scene *s, const vrt_scene_desc *d)
@@ -800,16 +787,16 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         const size_t sz_mats = s->mats.size() * sizeof(MatRec);
         const size_t sz_texs = std::max<size_t>(1, s->texs.size()) * sizeof(TexRec);
         const size_t sz_tex = (size_t)std::max<int64_t>(16, s->tex_bytes);
-        size_t off[12];
+        size_t off[11];
         size_t tot = 0;
-        const size_t sz_xnodes = VRT_NODE_BOX ? s->nodes.size() * sizeof(XNodeRec) : 0;
-        const size_t sizes[11] = { sz_nodes, sz_vox, sz_refs, sz_pos, sz_attr, sz_mats, sz_texs, sz_tex,
-                                   kQueueSlots * kQueueBytes, sz_nodes, sz_xnodes };
-        for (int i = 0; i < 11; ++i) {
+        const size_t sz_xnodes = s->nodes.size() * sizeof(XNodeRec);
+        const size_t sizes[10] = { sz_nodes, sz_vox, sz_refs, sz_pos, sz_attr, sz_mats, sz_texs, sz_tex,
+                                   kQueueSlots * kQueueBytes, sz_xnodes };
+        for (int i = 0; i < 10; ++i) {
                 off[i] = tot;
                 tot += align_up(sizes[i]);
         }
-        off[11] = tot;
+        off[10] = tot;
         HIPCHK(hipMalloc(&s->d_mem, tot));
         char *base = static_cast<char *>(s->d_mem);
         HIPCHK(hipMemset(base + off[8], 0, kQueueSlots * kQueueBytes));
@@ -836,17 +823,14 @@ static int upload(vrt_scene *s, const vrt_scene_desc *d)
         s->dev.tex_data = reinterpret_cast<const uint8_t *>(base + off[7]);
         s->d_queue = reinterpret_cast<uint32_t *>(base + off[8]);
         {
-                // the march copies of the nodes (DevScene::mnodes, xnodes)
+                // the march records of the nodes (DevScene::xnodes)
                 std::vector<XNodeRec> xn;
-                std::vector<NodeRec> mn = march_nodes(s, d, xn);
-                HIPCHK(hipMemcpy(base + off[9], mn.data(), sz_nodes, hipMemcpyHostToDevice));
-                s->dev.mnodes = reinterpret_cast<const NodeRec *>(base + off[9]);
+                march_nodes(s, d, xn);
                 if (sz_xnodes)
-                        HIPCHK(hipMemcpy(base + off[10], xn.data(), sz_xnodes, hipMemcpyHostToDevice));
-                s->dev.xnodes = reinterpret_cast<const XNodeRec *>(base + off[10]);
+                        HIPCHK(hipMemcpy(base + off[9], xn.data(), sz_xnodes, hipMemcpyHostToDevice));
+                s->dev.xnodes = reinterpret_cast<const XNodeRec *>(base + off[9]);
         }
         HIPCHK(persistent_blocks(&s->dev.persist_blocks, &s->dev.sec_blocks));
-        s->dev.nnodes = (int32_t)s->nodes.size();
         s->dev.grid_div = 1;
         s->dev.max_depth = s->max_depth;
         s->dev.nmat = (int32_t)s->mats.size();
@@ -1475,7 +1459,7 @@ static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int ra
         if (secondary_uses_queue(p.sc)) {
                 if (int rc = queue_take(s, st, &q, &slot))
                         return rc;
-                if (!VRT_SEC_COOP && !s_tri && !s_vox) {  // the occlusion walk: compaction
+                if (!s_tri && !s_vox) {  // the occlusion walk: compaction
                         const int64_t rays = deal_count(tile_deal(p.ntx, p.nty, nranks), rank) * 64 * (int64_t)spp;
                         if (int rc = spill_setup(s, rays, st, &sq, &set))
                                 return rc;
@@ -2201,22 +2185,9 @@ static int trace_ok(vrt_scene *s, float min_voxel)
         return VRT_OK;
 }
 
-// Split trace (primary pass -> one lane per cone -> film add) unless
-// VRT_TRACE_FUSED=1 selects the single fused kernel (A/B and tests).
-static bool trace_fused()
-{
-        static const bool f = [] {
-                const char *e = std::getenv("VRT_TRACE_FUSED");
-                return e && e[0] == '1';
-        }();
-        return f;
-}
-
 static int trace_scratch(vrt_scene *s, int set, const TraceParams &tp, TraceParams *out)
 {
         *out = tp;
-        if (trace_fused())
-                return VRT_OK;
         TraceSet &t = s->ts[set];
         const size_t nslots = (size_t)tp.r.tiles_this_rank * 256;
         // the primary pass's 64-B records, its deferred-sample count and list
@@ -2389,8 +2360,6 @@ extern "C" int vrt_trace_frame_device(vrt_scene *s, const vrt_camera *light_cam,
         tp0.r.out = d_out;
         if (int rc = trace_scratch(s, set, tp0, &tp))
                 return rc;
-        if (!tp.rec)
-                return fail(VRT_E_INVALID, "vrt_trace_frame_device needs the split trace (VRT_TRACE_FUSED unset)");
         unsigned int nhit = 0;
         auto overlap = [&]() -> int {
                 // the view's primary march beside the light pass (its records

@@ -39,23 +39,6 @@ struct alignas(16) XNodeRec {
 };
 static_assert(sizeof(XNodeRec) == 64, "XNodeRec must be 64 B");
 
-// The node triangle-box skip (internal nodes too, DevScene::xnodes):
-// 1 = the finite-slab walks read xnodes, 0 = mnodes (leaves only).
-// config 5 without per-ray ids: 1 = one pixel's rays walked as a pool of
-// subtree pieces (occl_pool, vrt_kernels.hip) instead of the ray compaction
-// (SpillQueues + resume round); measured 10 % slower (DESIGN appendix)
-#ifndef VRT_SEC_COOP
-#define VRT_SEC_COOP 0
-#endif
-// the compaction's resume: 1 = one round, its saved rays 64 to a wave walked
-// as a pool of subtree pieces (occl_pool) to the end; 0 = VRT_SEC_ROUNDS
-// rounds of one ray per lane
-#ifndef VRT_SEC_POOL_RESUME
-#define VRT_SEC_POOL_RESUME 1
-#endif
-#ifndef VRT_NODE_BOX
-#define VRT_NODE_BOX 1
-#endif
 
 // Leaf-list records, in leaf order with the vertices inlined (no dependent
 // index load in the leaf loop).  Two formats, chosen per scene:
@@ -122,21 +105,16 @@ struct DevScene {
         int32_t persist_blocks;  // resident 256-thread blocks of the persistent render on this
                                  // device (a multiple of 8), 0 = no persistent launches
         int32_t sec_blocks;      // the same for the persistent secondary-ray kernel
-        int32_t nnodes;          // node count (LDS node staging reads at most this many)
         int32_t grid_div;        // persistent render grid = resident slots / grid_div
                                  // (vrt_scene_set_frames_in_flight)
-        // March copy of the nodes: identical except that every non-root
-        // leaf holding triangles carries, instead of its voxel box, the
-        // union box of its triangles enlarged by lb_eps (leaf_box_ok).  A
-        // ray whose line misses it cannot pass intersect_triangle3 on any
-        // of them (which accepts a hit at any t), so the fast march skips
-        // the leaf's triangle loop; results are unchanged.  The skip is used
-        // for rays with every |o - lb_center| <= lb_reach, where lb_eps
-        // exceeds the fp32 rounding of the line test.
-        const NodeRec *mnodes;
-        // The same skip for every node (VRT_NODE_BOX): a subtree whose
-        // triangles' enlarged union box the line misses holds no leaf that
-        // can yield a record, so the walk does not expand it.
+        // March records of the nodes (XNodeRec): the node record and the
+        // union box of every triangle below it enlarged by lb_eps
+        // (leaf_box_ok).  A ray whose line misses that box cannot pass
+        // intersect_triangle3 (which accepts a hit at any t) on any triangle
+        // below the node, so the finite-slab walks skip the subtree (a leaf:
+        // its triangle loop); results are unchanged.  The skip is used for
+        // rays with every |o - lb_center| <= lb_reach, where lb_eps exceeds
+        // the fp32 rounding of the line test.
         const XNodeRec *xnodes;
         float lb_center[3];
         float lb_reach;
@@ -225,11 +203,10 @@ __host__ __device__ inline int slice_unit(int units, int x, int u, int ch)
 // wave walks one pixel's secondary rays until fewer than `t_first` of them
 // are still walking; it then stops, and each of those rays writes its walk
 // state -- the ray, the node it was about to visit next and its DFS stack --
-// to queue 0.  Resume round r (1..rounds) packs queue r-1's rays 64 to a
-// wave and continues their walks from the saved state, writing the rays
-// still walking below `t_next` lanes to queue r (the last round never
-// stops).  The walk after a resume is the walk that would have run, so
-// every ray's hit boolean is unchanged.  The pixel's count of hits and of
+// to queue 0.  The resume round (k_sec_stream, or k_sec_resume for films of
+// 2^26 pixels or more) continues their walks from the saved states, 64 rays
+// to a wave as one pool, to their ends.  The walk after a resume is the walk
+// that would have run, so every ray's hit boolean is unchanged.  The pixel's count of hits and of
 // rays still out lives in its unused primary-record word (prim[8*pix+7]);
 // the ray that brings the outstanding count to zero writes the pixel.
 // A queue is cut into chunks of kSpillChunk records: a wave takes a whole
@@ -259,8 +236,6 @@ struct SpillQueues {
         SpillRec *rec[2];    // queue r's records: rec[r & 1] + chunk * kSpillChunk
         uint32_t nchunks;    // chunks per queue; 0 = no compaction
         uint32_t t_first;    // phase-A threshold (walking lanes)
-        uint32_t t_next;     // threshold of resume rounds 1..rounds-1
-        int32_t rounds;      // resume launches
         int32_t stream;      // the resume round streams its rays (VRT_SEC_STREAM; films < 2^26 pixels)
 };
 

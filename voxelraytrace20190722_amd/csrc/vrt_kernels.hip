@@ -76,46 +76,6 @@ __device__ __forceinline__ void load_xnode(const XNodeRec *__restrict__ x, uint3
         tmx[0] = q2.w; tmx[1] = q3.x; tmx[2] = q3.y;
 }
 
-// LDS copy of the first kNS node records (the top BFS levels: node 0 is the
-// root, then whole levels in order), staged once per workgroup by
-// stage_nodes(); node i < kNS is read from it, the rest from HBM/L2.
-template <int kNS>
-__device__ __forceinline__ float4 *lds_node_table()
-{
-        __shared__ float4 t[kNS > 0 ? 2 * kNS : 1];
-        return t;
-}
-
-template <int kNS>
-__device__ __forceinline__ void stage_nodes(const NodeRec *__restrict__ nodes, int nnodes)
-{
-        if (kNS > 0) {
-                float4 *t = lds_node_table<kNS>();
-                const float4 *g = reinterpret_cast<const float4 *>(nodes);
-                const int n = 2 * (nnodes < kNS ? nnodes : kNS);
-                for (int i = threadIdx.x; i < n; i += blockDim.x)
-                        t[i] = g[i];
-                __syncthreads();
-        }
-}
-
-template <int kNS>
-__device__ __forceinline__ void load_node_st(const NodeRec *__restrict__ nodes, uint32_t i, float bmin[3],
-                                             float bmax[3], uint32_t &a, uint32_t &b)
-{
-        if (kNS > 0 && i < (uint32_t)kNS) {
-                const float4 *q = lds_node_table<kNS>() + 2 * i;
-                const float4 q0 = q[0];
-                const float4 q1 = q[1];
-                bmin[0] = q0.x; bmin[1] = q0.y; bmin[2] = q0.z;
-                bmax[0] = q0.w; bmax[1] = q1.x; bmax[2] = q1.y;
-                a = __float_as_uint(q1.z);
-                b = __float_as_uint(q1.w);
-        } else {
-                load_node(nodes, i, bmin, bmax, a, b);
-        }
-}
-
 // ---------------------------------------------------------------------------
 // Diagnostic build only (VRT_PHASE_STAMPS=1, never the product): per-wave
 // phase cycles (s_memtime) and lane activity of the fast march, summed over
@@ -456,10 +416,7 @@ __device__ __forceinline__ uint32_t expand_v1(const float bmin[3],
 // children ordered by two_slot_order / net4_order when no lane of the wave
 // has more than 2 / 4 of them (rank_order8 otherwise); the travorder
 // distances are finished only when some lane orders >= 2 children.
-// kStd >= 1: every lane's ray has tmin == +0 and tmax == FLT_MAX, so (fast
-// path, no NaN) `t >= tmin && t <= tmax` is exactly "t is +-0, +subnormal or
-// +normal" -- one v_cmp_class instead of two compares and an AND.
-// kStd == 2 (instead of the above): tmax == FLT_MAX, tmin is not NaN and
+// kStd == 2: tmax == FLT_MAX, tmin is not NaN and
 // every |dinv| <= 2^64 (no zero or tiny direction component), so with
 // |plane - o| < 2^61 (fast_ok) every slab distance is finite and the
 // reference's test !(t0 > t1) && (t0 in [tmin, FLT_MAX] || t1 in [tmin,
@@ -467,7 +424,7 @@ __device__ __forceinline__ uint32_t expand_v1(const float bmin[3],
 // from t1 >= tmin when t0 <= t1, and neither endpoint can be +inf), i.e.
 // max(t0, tmin) <= t1: tmin is folded into one axis's near distances once
 // per expansion, leaving max3, min3 and one compare per child.
-template <int kStd>
+template <int kStd>  // 0 or 2
 __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float bmax[3], const RayK &r, int &cnt,
                                               uint32_t content)
 {
@@ -511,15 +468,9 @@ __device__ __forceinline__ uint32_t expand_v2(const float bmin[3], const float b
                 bool h;
                 if (kStd == 2) {
                         h = t0 <= t1;  // t0 = max(near distances, 0)
-                } else {
-                        bool in0, in1;
-                        if (kStd) {
-                                in0 = __builtin_amdgcn_classf(t0, 0x1E0);  // -0, +0, +subnormal, +normal
-                                in1 = __builtin_amdgcn_classf(t1, 0x1E0);
-                        } else {
-                                in0 = (t0 >= r.tmin) & (t0 <= r.tmax);
-                                in1 = (t1 >= r.tmin) & (t1 <= r.tmax);
-                        }
+                } else {  // kStd == 0: the reference's range test
+                        const bool in0 = (t0 >= r.tmin) & (t0 <= r.tmax);
+                        const bool in1 = (t1 >= r.tmin) & (t1 <= r.tmax);
                         h = !(t0 > t1) & (in0 | in1);
                 }
                 hm |= (uint32_t)h << i;
@@ -624,24 +575,17 @@ __device__ __forceinline__ bool mt_record(const float4 q0, const float4 q1, cons
         const double det = e1x * px + e1y * py + e1z * pz;
         if (!(det > 0.000001) && !(det < -0.000001))
                 return false;  // parallel
-#ifndef VRT_MT_RECVT
-#define VRT_MT_RECVT 1
-#endif
         // small-leaf scenes: the origin is widened per record instead of
         // holding 6 VGPRs of doubles across the march (part of what lets the
         // persistent render run 6 waves per SIMD without spilling in its
         // advance loop; +3 % per frame); large-leaf scenes keep it hoisted
         // (their leaf loop dominates)
         float rox = r.o.x, roy = r.o.y, roz = r.o.z;
-        if (VRT_MT_RECVT && !kR64)
+        if (!kR64)
                 asm volatile("" : "+v"(rox), "+v"(roy), "+v"(roz));
         const double tx = (double)rox - v0x, ty = (double)roy - v0y, tz = (double)roz - v0z;
         const double uu = tx * px + ty * py + tz * pz;
         const bool pos = det > 0.000001;
-#ifndef VRT_LEAF_SIGNFOLD
-#define VRT_LEAF_SIGNFOLD 1
-#endif
-#if VRT_LEAF_SIGNFOLD
         // det < 0 branch folded onto the det > 0 one by negation (exact;
         // round-to-nearest is symmetric, so -(uu + vv) == (-uu) + (-vv)):
         // the same accept/reject decisions, without divergent sign branches
@@ -655,16 +599,6 @@ __device__ __forceinline__ bool mt_record(const float4 q0, const float4 q1, cons
         const double svv = pos ? vv : -vv;
         if (svv < 0.0 || suu + svv > sdet)
                 return false;
-#else
-        if (pos ? (uu < 0.0 || uu > det) : (uu > 0.0 || uu < det))
-                return false;
-        const double qx = ty * e1z - tz * e1y;
-        const double qy = tz * e1x - tx * e1z;
-        const double qz = tx * e1y - ty * e1x;
-        const double vv = dx * qx + dy * qy + dz * qz;
-        if (pos ? (vv < 0.0 || uu + vv > det) : (vv > 0.0 || uu + vv < det))
-                return false;
-#endif
         const double inv_det = 1.0 / det;
         const double t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
         // Triangle::isect (VRT/voxel_octree.cc:449-454)
@@ -699,10 +633,7 @@ __device__ __forceinline__ bool leaf_isect_v2(const void *__restrict__ refs,
 {
         bool any = false;
         float best = 0.f, best_t = 0.f;
-#ifndef VRT_LEAF_UNROLL
-#define VRT_LEAF_UNROLL 1
-#endif
-#pragma unroll VRT_LEAF_UNROLL
+#pragma unroll 1
         for (uint32_t k = 0; k < n; ++k) {
                 const float4 *q = kR64 ? reinterpret_cast<const float4 *>(static_cast<const RefRec64 *>(refs) + first + k)
                                        : reinterpret_cast<const float4 *>(static_cast<const RefRec48 *>(refs) + first + k);
@@ -733,14 +664,12 @@ __device__ __forceinline__ bool leaf_isect_v2(const void *__restrict__ refs,
 // not one load latency per record.  A/B at depth 6 (1080p primary): kG = 2
 // +3.7 %, 4 +3.4 %, 8 -17 % (SGPR spills); the light pass and the trace
 // render are unchanged (their longest waves are not bound by this chain).
-#ifndef VRT_UNI_GROUP
-#define VRT_UNI_GROUP 2
-#endif
+constexpr int kUniGroup = 2;
 template <bool kCount>
 __device__ __forceinline__ bool leaf_isect_uni(const RefRec64 *__restrict__ recs, uint32_t n, const RayK &r,
                                                MarchResult &m)
 {
-        constexpr int kG = VRT_UNI_GROUP;
+        constexpr int kG = kUniGroup;
         bool any = false;
         float best = 0.f, best_t = 0.f;
         uint32_t k = 0;
@@ -847,10 +776,7 @@ __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, u
 {
         if (kUni >= 2)
                 return leaf_isect_grp<(kUni >= 2 ? kUni : 2), kR64>(sc.refs, first, n, r, m);
-#ifndef VRT_LEAF_UNIFORM
-#define VRT_LEAF_UNIFORM 1
-#endif
-        if (kR64 && VRT_LEAF_UNIFORM && kUni && !kCount) {
+        if (kR64 && kUni && !kCount) {
                 // every active lane tests the same leaf (coherent rays,
                 // large leaves): the records' address and count are
                 // wave-uniform, so they come through the scalar cache.
@@ -858,19 +784,15 @@ __device__ __forceinline__ bool leaf_isect(const DevScene &sc, uint32_t first, u
                 // a few records per leaf the check costs more than it saves
                 const uint32_t f0 = __builtin_amdgcn_readfirstlane(first);
                 const uint32_t n0 = __builtin_amdgcn_readfirstlane(n);
-                if (__all(first == f0 && n == n0)) {
-                        if (VRT_UNI_GROUP > 1)
-                                return leaf_isect_uni<kCount>(static_cast<const RefRec64 *>(sc.refs) + f0, n0, r, m);
-                        return leaf_isect_v2<kCount, true>(static_cast<const RefRec64 *>(sc.refs) + f0, 0, n0,
-                                                           r, m);
-                }
+                if (__all(first == f0 && n == n0))
+                        return leaf_isect_uni<kCount>(static_cast<const RefRec64 *>(sc.refs) + f0, n0, r, m);
         }
         return leaf_isect_v2<kCount, kR64>(sc.refs, first, n, r, m);
 }
 
 // Does the ray's whole line (every t, as intersect_triangle3 accepts hits
 // behind the origin) meet the box?  The fast path's slab distances (finite:
-// fin_ok); used on DevScene::mnodes' enlarged triangle boxes of leaves.
+// fin_ok); used on DevScene::xnodes' enlarged triangle boxes.
 __device__ __forceinline__ bool line_meets_box(const float bmin[3], const float bmax[3], const RayK &r)
 {
         const float ax = (bmin[0] - r.o.x) * r.dinv.x, bx = (bmax[0] - r.o.x) * r.dinv.x;
@@ -881,7 +803,7 @@ __device__ __forceinline__ bool line_meets_box(const float bmin[3], const float 
         asm("v_min3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(fmaxf(ax, bx)), "v"(fmaxf(ay, by)), "v"(fmaxf(az, bz)));
         return t0 <= t1;
 }
-// the ray may skip leaves by their triangle boxes (DevScene::mnodes)
+// the ray may skip nodes by their triangle boxes (DevScene::xnodes)
 __device__ __forceinline__ bool leaf_box_ok(const DevScene &sc, const RayK &r)
 {
         return fabsf(r.o.x - sc.lb_center[0]) <= sc.lb_reach && fabsf(r.o.y - sc.lb_center[1]) <= sc.lb_reach &&
@@ -890,12 +812,12 @@ __device__ __forceinline__ bool leaf_box_ok(const DevScene &sc, const RayK &r)
 
 // gi::ray_march (VRT/voxel_octree.cc:131-188).  stk_* are this lane's LDS
 // stack columns (stride kBlock).  The finite-slab fast walk (kStd == 2)
-// reads DevScene::mnodes and skips a leaf whose triangles' box the ray's
-// line misses (no triangle of it can pass; the leaf is left as the reference
-// leaves it, with no record).
+// reads DevScene::xnodes and skips a node whose triangles' box the ray's
+// line misses (no triangle below it can pass; the reference visits it and
+// finds no record).
 // kBudget > 0: the walk gives up (m.deferred) before a leaf that would take
 // its triangle tests past kBudget; a caller re-walks such a ray elsewhere.
-template <bool kCount, bool kFast, int kS, int kStd, int kUni, bool kR64, int kNS = 0, int kBudget = 0>
+template <bool kCount, bool kFast, int kS, int kStd, int kUni, bool kR64, int kBudget = 0>
 __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                           uint2 *stk,
                                           uint32_t *stk_aux,
@@ -911,10 +833,10 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         float bmin[3], bmax[3];
         uint32_t a, b;
         constexpr bool kLB = kFast && kStd == 2 && !kCount;
-        constexpr bool kNB = kLB && VRT_NODE_BOX;  // every visited node by its triangle box
-        const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
+        constexpr bool kNB = kLB;  // every visited node by its triangle box
+        const NodeRec *__restrict__ nodes = sc.nodes;  // kNB: xnodes instead
         const bool lbok = kLB && __all(leaf_box_ok(sc, r));  // wave-uniform: held in SGPRs
-        load_node_st<kNS>(sc.nodes, 0, bmin, bmax, a, b);
+        load_node(sc.nodes, 0, bmin, bmax, a, b);
         if (!aabb_isect(bmin, bmax, r.o, r.dinv, r.tmin, r.tmax))
                 return;
         if (a & kLeafBit) {
@@ -933,10 +855,6 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
         uint32_t depth = 1;  // depth of the node whose children we walk
         uint32_t nexp = 1;
         int sp = 0;
-#ifndef VRT_WHILE_WHILE
-#define VRT_WHILE_WHILE 1
-#endif
-#if VRT_WHILE_WHILE
         // while-while: every lane first advances (pop / expand) to its next
         // non-empty leaf in DFS order, then the lanes test their leaves
         // together -- expand and leaf code no longer interleave per lane.
@@ -952,9 +870,6 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 uint32_t node = 0, nref = 0;
 #if VRT_PHASE_STAMPS
                 const unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifndef VRT_POP_VISIT
-#define VRT_POP_VISIT 1
 #endif
                 for (;;) {
 #if VRT_PHASE_STAMPS
@@ -976,11 +891,9 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                         fpos = x & 0xFFFFFFu;
                                         depth = x >> 24;
                                 }
-                                // VRT_POP_VISIT: a pushed entry always has
-                                // cnt > 0, so the popped level's next child is
-                                // visited in this same iteration
-                                if (!VRT_POP_VISIT)
-                                        continue;
+                                // a pushed entry always has cnt > 0, so the
+                                // popped level's next child is visited in this
+                                // same iteration
                         }
                         const uint32_t ci = order & 7u;
                         order >>= 3;
@@ -994,7 +907,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                 if (lbok && !line_meets_box(tmn, tmx, r))
                                         continue;  // no triangle below this node can pass
                         } else {
-                                load_node_st<kNS>(nodes, node, bmin, bmax, a, b);
+                                load_node(nodes, node, bmin, bmax, a, b);
                         }
                         if (!(a & kLeafBit)) {
                                 if (cnt) {
@@ -1014,8 +927,6 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         nref = a & ~kLeafBit;
                         if (nref == 0)
                                 continue;  // empty leaf (instrumented walk only)
-                        if (kLB && !kNB && lbok && !line_meets_box(bmin, bmax, r))
-                                continue;  // no triangle of this leaf can pass
                         leaf = true;
                         break;
                 }
@@ -1095,59 +1006,11 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 }
         }
 #endif
-#else
-        for (;;) {
-                if (cnt == 0) {
-                        if (sp == 0)
-                                break;
-                        --sp;
-                        const uint2 e = stk[sp * kS];
-                        base = e.x;
-                        const uint32_t w = e.y;
-                        order = w & 0xFFFFFFu;
-                        cnt = (int)(w >> 24);
-                        if (kCount) {
-                                const uint32_t x = stk_aux[sp * kS];
-                                fpos = x & 0xFFFFFFu;
-                                depth = x >> 24;
-                        }
-                        continue;
-                }
-                const uint32_t ci = order & 7u;
-                order >>= 3;
-                --cnt;
-                const uint32_t node = base + ci;
-                if (kCount)
-                        path_rem[depth * kS] = 7u - ((fpos >> (3 * ci)) & 7u);
-                load_node_st<kNS>(nodes, node, bmin, bmax, a, b);
-                if (!(a & kLeafBit)) {
-                        if (cnt) {
-                                stk[sp * kS] = make_uint2(base, order | ((uint32_t)cnt << 24));
-                                if (kCount)
-                                        stk_aux[sp * kS] = fpos | (depth << 24);
-                                ++sp;
-                        }
-                        order = expand<kCount, kFast, kStd>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
-                        base = a;
-                        ++depth;
-                        ++nexp;
-                        continue;
-                }
-                if (kCount)
-                        m.L++;
-                const uint32_t n = a & ~kLeafBit;
-                if (n && leaf_isect<kCount, kUni, kR64>(sc, b, n, r, m)) {
-                        m.hit = true;
-                        m.node = node;
-                        break;
-                }
-        }
         if (VRT_LIGHT_DIAG) {
                 m.A = dg_it;
                 m.L = dg_lp;
                 m.T = dg_tri;
         }
-#endif
         if (kCount) {
                 // 1 root test + 8 per expanded node, minus the children the
                 // reference never popped on the path it stopped on.
@@ -1188,44 +1051,33 @@ __device__ __forceinline__ bool fast_ok(const RayK &r)
 
 // expand_v2<2> / child_hit_mask<.., true> preconditions beyond fast_ok():
 // tmax = FLT_MAX, tmin not NaN, every |dinv| <= 2^64 (finite slab distances)
-#ifndef VRT_FIN
-#define VRT_FIN 1
-#endif
 __device__ __forceinline__ bool fin_ok(const RayK &r)
 {
         return r.tmax == kFltMax && !isnan(r.tmin) && fabsf(r.dinv.x) <= 0x1p64f && fabsf(r.dinv.y) <= 0x1p64f &&
                fabsf(r.dinv.z) <= 0x1p64f;
 }
 
-template <bool kCount, int kS, int kUni, bool kR64, int kNS = 0, int kBudget = 0>
+template <bool kCount, int kS, int kUni, bool kR64, int kBudget = 0>
 __device__ __forceinline__ void ray_march_dispatch(const DevScene &sc, const RayK &r,
                                                    uint2 *sb, uint32_t *sa, uint32_t *pr,
                                                    MarchResult &m)
 {
-#ifndef VRT_STD_RANGE
-#define VRT_STD_RANGE 1
-#endif
         if (__all(sc.fast_ok && fast_ok(r))) {
-                if (VRT_FIN && !kCount && __all(fin_ok(r)))
-                        ray_march<kCount, true, kS, 2, kUni, kR64, kNS, kBudget>(sc, r, sb, sa, pr, m);
-                else if (!VRT_FIN && VRT_STD_RANGE && __all(__float_as_uint(r.tmin) == 0u && r.tmax == kFltMax))
-                        ray_march<kCount, true, kS, 1, kUni, kR64, kNS, kBudget>(sc, r, sb, sa, pr, m);
+                if (!kCount && __all(fin_ok(r)))
+                        ray_march<kCount, true, kS, 2, kUni, kR64, kBudget>(sc, r, sb, sa, pr, m);
                 else
-                        ray_march<kCount, true, kS, 0, kUni, kR64, kNS, kBudget>(sc, r, sb, sa, pr, m);
+                        ray_march<kCount, true, kS, 0, kUni, kR64, kBudget>(sc, r, sb, sa, pr, m);
         } else
-                ray_march<kCount, false, kS, 0, kUni, kR64, kNS, kBudget>(sc, r, sb, sa, pr, m);
+                ray_march<kCount, false, kS, 0, kUni, kR64, kBudget>(sc, r, sb, sa, pr, m);
 }
 
 // True when ray_march's fast instantiation for camera rays is exact for
-// every lane of the wave: standard range (tmin = +0, tmax = FLT_MAX) and,
-// with VRT_FIN, finite slab distances (fin_ok).
-constexpr int kFastStd = VRT_FIN ? 2 : 1;
+// every lane of the wave: standard range (tmin = +0, tmax = FLT_MAX) and
+// finite slab distances (fin_ok).
+constexpr int kFastStd = 2;
 __device__ __forceinline__ bool wave_fast_std(const DevScene &sc, const RayK &r)
 {
-        bool ok = sc.fast_ok && fast_ok(r) && __float_as_uint(r.tmin) == 0u && r.tmax == kFltMax;
-        if (VRT_FIN)
-                ok = ok && fin_ok(r);
-        return __all(ok);
+        return __all(sc.fast_ok && fast_ok(r) && __float_as_uint(r.tmin) == 0u && r.tmax == kFltMax && fin_ok(r));
 }
 
 // ---------------------------------------------------------------------------
@@ -1397,8 +1249,8 @@ __device__ __forceinline__ int occl_walk(const DevScene &sc, const RayK &r, uint
         uint32_t a, b;
         // finite-slab walk: leaves skipped by their triangle boxes (as ray_march)
         constexpr bool kLB = kFast && kFin;
-        constexpr bool kNB = kLB && VRT_NODE_BOX;  // every visited node by its triangle box
-        const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
+        constexpr bool kNB = kLB;  // every visited node by its triangle box
+        const NodeRec *__restrict__ nodes = sc.nodes;  // kNB: xnodes instead
         const bool lbok = kLB && __all(leaf_box_ok(sc, r));  // wave-uniform: held in SGPRs
         const uint32_t s = dir_signs(r);
         uint32_t mask = w.mask;
@@ -1421,9 +1273,7 @@ __device__ __forceinline__ int occl_walk(const DevScene &sc, const RayK &r, uint
                                 --sp;
                                 const uint2 e = stk[sp * kS];
                                 base = e.x;
-                                mask = e.y;
-                                if (!VRT_POP_VISIT)  // pushed masks are non-zero: visit now
-                                        continue;
+                                mask = e.y;  // pushed masks are non-zero: visit now
                         }
                         const uint32_t ci = (uint32_t)__builtin_ctz(mask) ^ s;
                         mask &= mask - 1u;
@@ -1445,17 +1295,12 @@ __device__ __forceinline__ int occl_walk(const DevScene &sc, const RayK &r, uint
                                 continue;
                         }
                         nref = a & ~kLeafBit;  // > 0: the content mask skips empty leaves
-                        if (kLB && !kNB && lbok && !line_meets_box(bmin, bmax, r))
-                                continue;  // no triangle of this leaf can pass
                         leaf = true;
                         break;
                 }
                 if (!leaf)
                         return kOcclMiss;
-#ifndef VRT_SEC_UNI
-#define VRT_SEC_UNI 1
-#endif
-                if (kR64 && VRT_SEC_UNI) {
+                if (kR64) {
                         // large leaves: when every active lane tests the same
                         // leaf (rays of one origin), the records come through
                         // the scalar cache (as leaf_isect)
@@ -1485,14 +1330,11 @@ __device__ __forceinline__ bool ray_occluded(const DevScene &sc, const RayK &r, 
 template <int kS, bool kR64>
 __device__ __forceinline__ bool ray_occluded_dispatch(const DevScene &sc, const RayK &r, uint2 *stk)
 {
-        // VRT_FIN: the fast walk is the finite-distance one (child_hit_mask's
-        // kFin); a wave with a ray outside it (a tiny or zero direction
-        // component, tmax != FLT_MAX, a NaN tmin) takes the exact walk
-        bool ok = sc.fast_ok && fast_ok(r);
-        if (VRT_FIN)
-                ok = ok && fin_ok(r);
-        if (__all(ok))
-                return ray_occluded<true, kS, kR64, VRT_FIN != 0>(sc, r, stk);
+        // the fast walk is the finite-distance one (child_hit_mask's kFin); a
+        // wave with a ray outside it (a tiny or zero direction component,
+        // tmax != FLT_MAX, a NaN tmin) takes the exact walk
+        if (__all(sc.fast_ok && fast_ok(r) && fin_ok(r)))
+                return ray_occluded<true, kS, kR64, true>(sc, r, stk);
         return ray_occluded<false, kS, kR64>(sc, r, stk);
 }
 
@@ -1506,16 +1348,13 @@ template <int kS, bool kR64>
 __device__ __forceinline__ int occl_dispatch_spill(const DevScene &sc, const RayK &r, uint2 *stk, OcclState &w,
                                                    bool resume, uint32_t spill_t)
 {
-        bool ok = sc.fast_ok && fast_ok(r);
-        if (VRT_FIN)
-                ok = ok && fin_ok(r);
-        if (__all(ok)) {
+        if (__all(sc.fast_ok && fast_ok(r) && fin_ok(r))) {
                 if (!resume) {
-                        const int st = occl_start<true, kR64, VRT_FIN != 0>(sc, r, w);
+                        const int st = occl_start<true, kR64, true>(sc, r, w);
                         if (st != kOcclWalk)
                                 return st;
                 }
-                return occl_walk<true, kS, kR64, VRT_FIN != 0, true>(sc, r, stk, w, spill_t);
+                return occl_walk<true, kS, kR64, true, true>(sc, r, stk, w, spill_t);
         }
         if (!resume) {
                 const int st = occl_start<false, kR64>(sc, r, w);
@@ -1545,8 +1384,8 @@ __device__ __forceinline__ int occl_dispatch_spill(const DevScene &sc, const Ray
 // slab, box and MT tests are occl_walk's, so every ray's boolean is
 // unchanged; only work after a ray's first passing leaf differs (pieces of
 // it walked in parallel until the bit is seen at their next leaf).
-// Used for the resume round of the compaction (VRT_SEC_POOL_RESUME: 64 saved
-// rays of unrelated pixels) and, with VRT_SEC_COOP, for whole pixels.
+// Used for the resume round of the compaction (64 saved rays of unrelated
+// pixels).
 // dirs: [64][3] slot directions (LDS); opix: slot -> pixel (LDS, kSlotOrigin;
 // origin = prim[8 pix + 1..3]); mbox: 64 uint2 (LDS); hword: one 64-bit LDS
 // word; stk: this lane's LDS stack column (stride kS) holding its initial
@@ -1570,8 +1409,8 @@ __device__ __forceinline__ uint64_t occl_pool(const DevScene &sc, f3 o, const fl
                                               uint32_t mask, int sp, uint64_t hitm)
 {
         constexpr bool kLB = kFast && kFin;
-        constexpr bool kNB = kLB && VRT_NODE_BOX;
-        const NodeRec *__restrict__ nodes = kLB ? sc.mnodes : sc.nodes;
+        constexpr bool kNB = kLB;
+        const NodeRec *__restrict__ nodes = sc.nodes;  // kNB: xnodes instead
         const uint32_t lane = lane_id();
         uint32_t slot = lane;
         RayK r = pool_ray<kSlotOrigin>(o, prim, opix, dirs, slot, tmin);
@@ -1640,8 +1479,6 @@ __device__ __forceinline__ uint64_t occl_pool(const DevScene &sc, f3 o, const fl
                                         const uint2 e = stk[sp * kS];
                                         base = e.x;
                                         mask = e.y;
-                                        if (!VRT_POP_VISIT)
-                                                continue;
                                 }
                                 const uint32_t ci = (uint32_t)__builtin_ctz(mask) ^ s;
                                 mask &= mask - 1u;
@@ -1663,8 +1500,6 @@ __device__ __forceinline__ uint64_t occl_pool(const DevScene &sc, f3 o, const fl
                                         continue;
                                 }
                                 nref = a & ~kLeafBit;
-                                if (kLB && !kNB && lbok && !line_meets_box(bmin, bmax, r))
-                                        continue;
                                 leaf = true;
                                 break;
                         }
@@ -1676,7 +1511,7 @@ __device__ __forceinline__ uint64_t occl_pool(const DevScene &sc, f3 o, const fl
                 bool hit = false;
                 if (leaf) {
                         bool done = false;
-                        if (kR64 && VRT_SEC_UNI) {
+                        if (kR64) {
                                 const uint32_t f0 = __builtin_amdgcn_readfirstlane(b);
                                 const uint32_t n0 = __builtin_amdgcn_readfirstlane(nref);
                                 if (__all(b == f0 && nref == n0)) {
@@ -1839,14 +1674,10 @@ __device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
 }
 
 // ---------------------------------------------------------------------------
-// Primary render: an 8x8 tile = 4 waves of 4x4 pixels x 4 samples, run as
-// VRT_RENDER_WAVES waves per workgroup (4: one workgroup per tile; 1: one
-// wave per workgroup, so a finished wave frees its slot and LDS at once).
+// Primary render: an 8x8 tile = 4 waves of 4x4 pixels x 4 samples, one wave
+// per workgroup (a finished wave frees its slot and LDS at once).
 // ---------------------------------------------------------------------------
-#ifndef VRT_RENDER_WAVES
-#define VRT_RENDER_WAVES 1
-#endif
-constexpr int kRenderBlock = 64 * VRT_RENDER_WAVES;
+constexpr int kRenderBlock = 64;
 // One work unit of the primary render: the 4x4-pixel quadrant `wave` of
 // this rank's k-th 8x8 tile, 4 gen_rays4 samples per pixel, one ray per
 // lane (lane = 4*pixel + sample).  stk_* are this lane's LDS stack columns.
@@ -1855,8 +1686,7 @@ constexpr int kRenderBlock = 64 * VRT_RENDER_WAVES;
 // standard-range instantiation is compiled in (fewer live registers); a wave
 // whose rays need another path returns false before writing anything and the
 // caller defers the unit to k_render_defer.
-template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kNS = 0,
-          int kBudget = 0>
+template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kBudget = 0>
 __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wave, int lane, uint2 *stk,
                                             uint32_t *stk_aux, uint32_t *path_rem)
 {
@@ -1915,9 +1745,9 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         if (kFastOnly) {
                 if (!wave_fast_std(p.sc, r) || (p.test_flags & VRT_TEST_FORCE_DEFER))
                         return false;
-                ray_march<false, true, kS, kFastStd, true, kR64, kNS, kBudget>(p.sc, r, stk, nullptr, nullptr, m);
+                ray_march<false, true, kS, kFastStd, true, kR64, kBudget>(p.sc, r, stk, nullptr, nullptr, m);
         } else {
-                ray_march_dispatch<kCount, kS, true, kR64, kNS>(p.sc, r, stk, stk_aux, path_rem, m);
+                ray_march_dispatch<kCount, kS, true, kR64>(p.sc, r, stk, stk_aux, path_rem, m);
         }
 #if VRT_UNIT_DIAG && VRT_LIGHT_DIAG
         if (kFastOnly) {
@@ -1927,17 +1757,11 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                         g_unit_walk[(size_t)ku * 4 + lane] = lane == 0 ? v[0] : lane == 1 ? v[1] : lane == 2 ? v[2] : v[3];
         }
 #endif
-        // persistent kernels: the pixel (and with VRT_REDIR the direction)
-        // are made again -- the same operations, so the same bits -- rather
-        // than held live across the march
-#ifndef VRT_REDIR
-#define VRT_REDIR 0
-#endif
-        if (!kSamples) {
-                const f3 d2 = sample_of(lane_now(), px, py, s, lx, ly);
-                if (VRT_REDIR)
-                        dn = d2;
-        }
+        // persistent kernels: the pixel is made again -- the same
+        // operations, so the same bits -- rather than held live across the
+        // march
+        if (!kSamples)
+                (void)sample_of(lane_now(), px, py, s, lx, ly);
 
         // kBudget: a pixel with a sample whose walk hit the budget is left to
         // k_render_tail (all 4 samples re-walked there, 8 lanes per ray)
@@ -2022,7 +1846,7 @@ __global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k
         // XCD-aware order: blocks b, b+8, ... run on one XCD; give them
         // consecutive work units (a unit = kUnitsPerTile-th of an 8x8 tile)
         // so each XCD's L2 serves one screen region.
-        constexpr int kQ = 4 / VRT_RENDER_WAVES;  // units per tile
+        constexpr int kQ = 4;  // units per tile
         const int nb = gridDim.x;
         const int b = blockIdx.x;
         const int per = (nb + 7) >> 3;
@@ -2035,7 +1859,7 @@ __global__ __launch_bounds__(kRenderBlock, kCount ? 1 : VRT_WAVES_PER_EU) void k
         if (u >= p.tiles_this_rank * kQ)
                 return;
         const int k = u / kQ;
-        const int wave = (u % kQ) * VRT_RENDER_WAVES + (tid >> 6), lane = tid & 63;
+        const int wave = (u % kQ) + (tid >> 6), lane = tid & 63;
         render_unit<kCount, kR64, kB>(p, k, wave, lane, stk + tid, stk_aux + (kCount ? tid : 0),
                                       path_rem + (kCount ? tid : 0));
 }
@@ -2057,7 +1881,7 @@ __device__ __forceinline__ uint32_t take_unit(uint32_t *ctr)
 // workgroups sized to fill the chip once; every wave pulls quadrant units
 // from a per-XCD counter (blocks b, b+8, ... share an XCD and its L2; an
 // XCD's counter covers one contiguous slice of the tiles) and, once its own
-// slice is exhausted, from the other XCDs' counters (VRT_PERSIST_HELP).
+// slice is exhausted, from the other XCDs' counters.
 // One-wave workgroups top out at 16 resident waves per CU (the per-CU
 // workgroup limit); at VRT_PERSIST_WAVES_PER_EU = 5 this kernel keeps 5
 // waves per SIMD = 20 per CU resident, and a wave never waits for a
@@ -2067,7 +1891,6 @@ __device__ __forceinline__ uint32_t take_unit(uint32_t *ctr)
 // fast standard-range march is compiled in; a wave with a ray that needs the
 // exact path (a non-zero denormal direction component) appends its unit to
 // the launch's deferred list, which k_render_defer renders afterwards.
-// kNS > 0: the first kNS node records are staged in LDS (VRT_LDS_NODES).
 constexpr int kPersistBlock = 256;
 // Block slots (256 threads, 4 waves each) a persistent launch for one rank of
 // a multi-GPU frame leaves free, so the RCCL kernel moving the previous frame
@@ -2078,48 +1901,17 @@ constexpr int kCollectiveReserve = 32;
 #ifndef VRT_PERSIST_WAVES_PER_EU
 #define VRT_PERSIST_WAVES_PER_EU 6
 #endif
-#ifndef VRT_PERSIST_HELP
-#define VRT_PERSIST_HELP 1
-#endif
-#ifndef VRT_LDS_NODES
-#define VRT_LDS_NODES 0
-#endif
-// 1: a wave reads another slice's counter before adding to it and skips a
-// drained slice, so a wave makes one failing add (its own slice) instead of
-// eight; the adds are then no longer a fixed count, so the launch's last wave
-// (kRenderDoneWord) zeroes the counters and the host resets the slot's bases
-// (queue_release with waves < 0)
-#ifndef VRT_Q_PRECHECK
-#define VRT_Q_PRECHECK 0
-#endif
-// 1: a wave whose own slice is drained (the launch's tail: it helps the other
-// XCDs' slices) raises its issue priority, so with frames in flight the tail
-// of frame k runs ahead of frame k+1's bulk waves on the same SIMDs
-#ifndef VRT_TAIL_PRIO
-#define VRT_TAIL_PRIO 0
-#endif
-constexpr int kRenderDoneWord = kDeferDoneWord + 16;  // in WorkQueue::defer (the deferred pass's line)
 template <bool kFastOnly, int kBudget = 0>
 __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_render_p(RenderParams p)
 {
-        constexpr int kNS = kFastOnly ? VRT_LDS_NODES : 0;
         __shared__ uint2 stk[kStack * kPersistBlock];
-        stage_nodes<kNS>(p.sc.mnodes, p.sc.nnodes);  // = nodes for internal nodes and the root
         const int tid = threadIdx.x, lane = tid & 63;
         const int xcd = blockIdx.x & 7;
-        for (int j = 0; j < (VRT_PERSIST_HELP ? 8 : 1); ++j) {
+        for (int j = 0; j < 8; ++j) {
                 const int x = (xcd + j) & 7;
                 const int units = p.tiles_this_rank * 4, n = slice_size(units, x, VRT_SLICE_CHUNK);
                 if (n <= 0)
                         continue;
-                if (VRT_TAIL_PRIO && j == 1)
-                        __builtin_amdgcn_s_setprio(2);
-                if (VRT_Q_PRECHECK && j > 0) {
-                        const uint32_t c = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                p.q.ctr + x * kQueueStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                        if (c - p.q.base[x] >= (uint32_t)n)
-                                continue;
-                }
                 for (;;) {
                         const uint32_t u = take_unit(p.q.ctr + x * kQueueStride) - p.q.base[x];
                         if (u >= (uint32_t)n)
@@ -2131,7 +1923,7 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
 #if VRT_UNIT_DIAG
                         const uint32_t dg_u0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kNS, kBudget>(
+                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kBudget>(
                                 p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr);
 #if VRT_UNIT_DIAG
                         {
@@ -2162,19 +1954,6 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
                                                 p.q.defer[kDeferList + x * kDeferSliceCap + d] = (uint32_t)kq;
                                 }
                         }
-                }
-        }
-        if (VRT_Q_PRECHECK) {
-                // every counter add of this wave has returned (each take's
-                // value was used) before this add: the last wave to get here
-                // sees no later add and zeroes the counters for the slot's
-                // next launch
-                const uint32_t fin = take_unit(p.q.defer + kRenderDoneWord);
-                if (fin == gridDim.x * (uint32_t)(kPersistBlock / 64) - 1u) {
-#pragma unroll
-                        for (int x = 0; x < 8; ++x)
-                                p.q.ctr[x * kQueueStride] = 0u;
-                        p.q.defer[kRenderDoneWord] = 0u;
                 }
         }
 }
@@ -2450,13 +2229,6 @@ struct SecondaryParams {
         SpillQueues sq;        // ray compaction (kAny, persistent launch); sq.nchunks == 0: off
 };
 
-#ifndef VRT_SEC_WAVES
-#define VRT_SEC_WAVES 1
-#endif
-#ifndef VRT_SEC_WAVES_PER_EU
-#define VRT_SEC_WAVES_PER_EU 6
-#endif
-constexpr int kSecBlock = 64 * VRT_SEC_WAVES;
 // the persistent config-5 kernels (k_secondary_p, k_sec_resume): 4-wave workgroups
 constexpr int kSecPBlock = 256;
 #ifndef VRT_SECP_WAVES_PER_EU
@@ -2470,8 +2242,7 @@ constexpr int kSecPBlock = 256;
 // ray's hit boolean -> the occlusion walk (ray_occluded), same booleans.
 template <bool kR64, bool kAny, int kS>
 __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_t k, int lane, uint2 *stk,
-                                                float (*pts)[3], uint2 *mbox, unsigned long long *hword,
-                                                SpillCursor &cur)
+                                                float (*pts)[3], SpillCursor &cur)
 {
         // lane id re-read per pixel (not held across k_secondary_p's loop)
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
@@ -2523,51 +2294,6 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (kAny && VRT_SEC_COOP) {
-                // the pixel's rays as one pool of subtree walks (occl_pool):
-                // directions into LDS (over the sphere points), then the
-                // fast / exact walk chosen for the whole pixel
-                bool ok = true;
-                RayK r;
-                if (lane < p.spp) {
-                        const f3 d = normalize(nrm + mk3(pts[lane][0], pts[lane][1], pts[lane][2]));
-                        pts[lane][0] = d.x;
-                        pts[lane][1] = d.y;
-                        pts[lane][2] = d.z;
-                        r = make_rayk(hp, d, p.res, kFltMax);
-                        ok = p.sc.fast_ok && fast_ok(r) && (!VRT_FIN || fin_ok(r));
-                }
-                wave_lds_sync();
-                OcclState w;
-                w.base = w.mask = 0;
-                bool busy = false, hit = false;
-                uint64_t hm;
-                if (__all(ok)) {
-                        if (lane < p.spp) {
-                                const int st = occl_start<true, kR64, VRT_FIN != 0>(p.sc, r, w);
-                                busy = st == kOcclWalk;
-                                hit = st == kOcclHit;
-                        }
-                        hm = occl_pool<true, kS, kR64, VRT_FIN != 0, false>(p.sc, hp, nullptr, nullptr, p.res, pts,
-                                                                             mbox, hword, stk, busy, w.base, w.mask,
-                                                                             0, __ballot(hit));
-                } else {
-                        if (lane < p.spp) {
-                                const int st = occl_start<false, kR64>(p.sc, r, w);
-                                busy = st == kOcclWalk;
-                                hit = st == kOcclHit;
-                        }
-                        hm = occl_pool<false, kS, kR64, false, false>(p.sc, hp, nullptr, nullptr, p.res, pts, mbox,
-                                                                      hword, stk, busy, w.base, w.mask, 0,
-                                                                      __ballot(hit));
-                }
-                if (p.s_hit && lane < p.spp)
-                        p.s_hit[vi * (size_t)p.spp + lane] = (int32_t)((hm >> lane) & 1ull);
-                if (lane == 0)
-                        p.vis[vi] = (float)(p.spp - (int)__popcll(hm)) / (float)p.spp;
-                wave_lds_sync();  // pts / mbox / hword are rewritten by the next pixel
-                return;
-        }
         // with compaction: the rays still walking when fewer than t_first
         // lanes are go to queue 0 (SpillQueues)
         const uint32_t t = kAny ? spill_reserve(p.sq, p.sq.ctr, p.sq.fill[0], cur, p.sq.t_first) : 0u;
@@ -2606,11 +2332,10 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         }
 }
 
-// Resume round p.round of the compaction (SpillQueues): queue round-1's rays,
-// 64 to a wave in append order, walk on from their saved states; a ray that
-// ends adds to its pixel's counts (prim[8*pix+7]: hits << 8 | rays out) and
-// the one that brings the rays out to zero writes the pixel; below t_next
-// walking lanes (not in the last round) a ray goes to queue round.
+// The resume round of the compaction (SpillQueues): queue 0's rays walk on
+// from their saved states to their ends; a ray that ends adds to its pixel's
+// counts (prim[8*pix+7]: hits << 8 | rays out) and the one that brings the
+// rays out to zero writes the pixel.
 struct ResumeParams {
         DevScene sc;
         float *prim;
@@ -2618,63 +2343,12 @@ struct ResumeParams {
         int32_t *s_hit;
         int32_t spp;
         float res;
-        int32_t round;
         int32_t nx, W8;  // pixel index <-> primary record index (VRT_SEC_STREAM)
         int32_t test_flags;
         SpillQueues sq;
 };
 
-// One chunk of queue round-1: its rays 64 at a time, each walk continued
-// from its record; rays that end update their pixel, rays stopped again (t >
-// 0, not the last round) go to queue round.
-template <bool kR64>
-__device__ __forceinline__ void resume_chunk(const ResumeParams &p, const SpillRec *rec, uint32_t fill, uint32_t t,
-                                             SpillCursor &cur, uint2 *stk)
-{
-        uint32_t *cout = p.sq.ctr + p.round * kSpillCtrStride;
-        uint32_t *fout = p.sq.fill[p.round & 1];
-        for (uint32_t g = 0; g < fill; g += 64) {
-                const uint32_t tg = spill_reserve(p.sq, cout, fout, cur, t);
-                int lane;
-                asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-                const uint32_t i = g + (uint32_t)lane;
-                bool spilled = false;
-                OcclState w;
-                f3 dn;
-                uint4 h0 = make_uint4(0u, 0u, 0u, 0u);
-                if (i < fill) {
-                        const SpillRec *q = rec + i;
-                        h0 = reinterpret_cast<const uint4 *>(q)[0];
-                        const uint4 h1 = reinterpret_cast<const uint4 *>(q)[1];
-                        const uint4 h2 = reinterpret_cast<const uint4 *>(q)[2];
-                        w.sp = (int)h0.w;
-                        w.base = h2.x;
-                        w.mask = h2.y;
-                        const uint2 *e = reinterpret_cast<const uint2 *>(q->stk);
-                        for (int k = 0; k < w.sp; ++k)
-                                stk[k * kSecPBlock] = e[k];
-                        float *pr = p.prim + 8 * (size_t)h0.x;
-                        const f3 hp = mk3(pr[1], pr[2], pr[3]);
-                        dn = mk3(__uint_as_float(h1.x), __uint_as_float(h1.y), __uint_as_float(h1.z));
-                        const RayK r = make_rayk(hp, dn, p.res, kFltMax);
-                        const int res = occl_dispatch_spill<kSecPBlock, kR64>(p.sc, r, stk, w, true, tg);
-                        spilled = res == kOcclSpill;
-                        if (!spilled) {
-                                const uint32_t hit = res == kOcclHit ? 1u : 0u;
-                                if (p.s_hit)
-                                        p.s_hit[(size_t)h0.y * (size_t)p.spp + h0.z] = (int32_t)hit;
-                                const uint32_t old =
-                                        atomicAdd(reinterpret_cast<uint32_t *>(pr) + 7, hit ? 255u : 0xFFFFFFFFu);
-                                if ((old & 0xFFu) == 1u)  // the pixel's last ray
-                                        p.vis[h0.y] = (float)(p.spp - (int)((old >> 8) + hit)) / (float)p.spp;
-                        }
-                }
-                if (tg)
-                        spill_group<kSecPBlock>(p.sq.rec[p.round & 1], cur, spilled, h0.x, h0.y, h0.z, dn, w, stk);
-        }
-}
-
-// VRT_SEC_POOL_RESUME: one chunk of queue 0, its rays 64 at a time as one
+// One chunk of queue 0 (or a 64-ray piece of it): its rays 64 at a time as one
 // pool (occl_pool with each slot's origin its pixel's primary hit point), each
 // batch walked to the end; then lane j reports slot j's ray to its pixel.
 template <bool kR64>
@@ -2704,7 +2378,7 @@ __device__ __forceinline__ void resume_pool_chunk(const ResumeParams &p, const S
                         dn = mk3(__uint_as_float(h1.x), __uint_as_float(h1.y), __uint_as_float(h1.z));
                         const float *pr = p.prim + 8 * (size_t)h0.x;
                         const RayK r = make_rayk(mk3(pr[1], pr[2], pr[3]), dn, p.res, kFltMax);
-                        ok = p.sc.fast_ok && fast_ok(r) && (!VRT_FIN || fin_ok(r));
+                        ok = p.sc.fast_ok && fast_ok(r) && fin_ok(r);
                         busy = true;
                 }
                 dirs[lane][0] = dn.x;
@@ -2713,7 +2387,7 @@ __device__ __forceinline__ void resume_pool_chunk(const ResumeParams &p, const S
                 opix[lane] = h0.x;
                 wave_lds_sync();
                 const uint64_t hm =
-                        __all(ok) ? occl_pool<true, kSecPBlock, kR64, VRT_FIN != 0, true>(
+                        __all(ok) ? occl_pool<true, kSecPBlock, kR64, true, true>(
                                             p.sc, mk3(0.f, 0.f, 0.f), p.prim, opix, p.res, dirs, mbox, hword, stk,
                                             busy, base, mask, sp, 0ull)
                                   : occl_pool<false, kSecPBlock, kR64, false, true>(
@@ -2775,7 +2449,7 @@ __device__ __forceinline__ bool stream_chunk_fast(const ResumeParams &p, const S
                 const RayK r = make_rayk(mk3(pr[1], pr[2], pr[3]),
                                          mk3(__uint_as_float(h1.x), __uint_as_float(h1.y), __uint_as_float(h1.z)),
                                          p.res, kFltMax);
-                ok = ok && p.sc.fast_ok && fast_ok(r) && (!VRT_FIN || fin_ok(r)) && (!VRT_FIN || leaf_box_ok(p.sc, r));
+                ok = ok && p.sc.fast_ok && fast_ok(r) && fin_ok(r) && leaf_box_ok(p.sc, r);
         }
         return __all(ok);
 }
@@ -2786,10 +2460,10 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
                                               float (*dirs)[3], uint32_t *sinfo, uint2 *mbox,
                                               unsigned long long *hword)
 {
-        constexpr bool kFin = VRT_FIN != 0;
-        constexpr bool kNB = kFin && VRT_NODE_BOX;
+        constexpr bool kFin = true;
+        constexpr bool kNB = kFin;
         const DevScene &sc = p.sc;
-        const NodeRec *__restrict__ nodes = kFin ? sc.mnodes : sc.nodes;
+        const NodeRec *__restrict__ nodes = sc.nodes;  // kNB: xnodes instead
         const uint32_t lane = lane_id();
         const uint64_t lt = (1ull << lane) - 1ull;
         uint64_t assigned = 0;  // wave-uniform: slots holding a ray
@@ -2935,8 +2609,6 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
                                         const uint2 e = stk[sp * kSecPBlock];
                                         base = e.x;
                                         mask = e.y;
-                                        if (!VRT_POP_VISIT)
-                                                continue;
                                 }
                                 const uint32_t ci = (uint32_t)__builtin_ctz(mask) ^ s;
                                 mask &= mask - 1u;
@@ -2958,8 +2630,6 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
                                         continue;
                                 }
                                 nref = a & ~kLeafBit;
-                                if (kFin && !kNB && !line_meets_box(bmin, bmax, r))
-                                        continue;
                                 leaf = true;
                                 break;
                         }
@@ -2971,7 +2641,7 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
                 bool hit = false;
                 if (leaf) {
                         bool done = false;
-                        if (kR64 && VRT_SEC_UNI) {
+                        if (kR64) {
                                 const uint32_t f0 = __builtin_amdgcn_readfirstlane(b);
                                 const uint32_t n0 = __builtin_amdgcn_readfirstlane(nref);
                                 if (__all(b == f0 && nref == n0)) {
@@ -3038,24 +2708,22 @@ template <bool kR64>
 __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_resume(ResumeParams p)
 {
         __shared__ uint2 stk[kStack * kSecPBlock];
-        __shared__ float dirs[VRT_SEC_POOL_RESUME ? kSecPBlock / 64 : 1][64][3];
-        __shared__ uint32_t opix[VRT_SEC_POOL_RESUME ? kSecPBlock / 64 : 1][64];
-        __shared__ uint2 mbox[VRT_SEC_POOL_RESUME ? kSecPBlock / 64 : 1][64];
+        __shared__ float dirs[kSecPBlock / 64][64][3];
+        __shared__ uint32_t opix[kSecPBlock / 64][64];
+        __shared__ uint2 mbox[kSecPBlock / 64][64];
         __shared__ unsigned long long hword[kSecPBlock / 64];
         const int tid = threadIdx.x;
-        uint32_t *cin = p.sq.ctr + (p.round - 1) * kSpillCtrStride;
-        const uint32_t n = min(cin[0], p.sq.nchunks);  // queue round-1's chunks (earlier launches)
-        const uint32_t *fin = p.sq.fill[(p.round - 1) & 1];
-        const SpillRec *in = p.sq.rec[(p.round - 1) & 1];
-        const uint32_t t = p.round < p.sq.rounds ? p.sq.t_next : 0u;
-        SpillCursor cur;
-        cur.chunk = kSpillNone;
-        cur.fill = 0;
+        uint32_t *cin = p.sq.ctr;
+        const uint32_t n = min(cin[0], p.sq.nchunks);  // queue 0's chunks (the walk launch's)
+        const uint32_t *fin = p.sq.fill[0];
+        const SpillRec *in = p.sq.rec[0];
         // leftover mode (after k_sec_stream): the chunks it listed, from ctr[4],
         // each as kSpillChunk / 64 pieces of 64 rays on different waves (the
         // few leftover chunks of a frame would otherwise leave one wave
-        // walking a whole chunk's batches one after the other)
-        const bool left = VRT_SEC_POOL_RESUME && p.sq.stream;
+        // walking a whole chunk's batches one after the other); otherwise
+        // (films of 2^26 pixels or more, whose pixel index does not fit
+        // resume_stream's slot word) every chunk of queue 0 whole
+        const bool left = p.sq.stream;
         constexpr uint32_t kParts = kSpillChunk / 64;
         const uint32_t nl = left ? p.sq.ctr[3] * kParts : 0u;
         for (;;) {
@@ -3071,36 +2739,14 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_resum
                         if (c >= n)
                                 break;
                 }
-                if (VRT_SEC_POOL_RESUME) {
-                        const int w = VRT_SEC_POOL_RESUME ? tid >> 6 : 0;
-                        const uint32_t f = fin[c], lo = part * 64u;
-                        if (lo >= f)
-                                continue;
-                        const uint32_t cnt = left ? min(64u, f - lo) : f;
-                        resume_pool_chunk<kR64>(p, in + (size_t)c * kSpillChunk + lo, cnt, stk + tid, dirs[w],
-                                                opix[w], mbox[w], hword + (tid >> 6));
-                } else {
-                        resume_chunk<kR64>(p, in + (size_t)c * kSpillChunk, fin[c], t, cur, stk + tid);
-                }
+                const int w = tid >> 6;
+                const uint32_t f = fin[c], lo = part * 64u;
+                if (lo >= f)
+                        continue;
+                const uint32_t cnt = left ? min(64u, f - lo) : f;
+                resume_pool_chunk<kR64>(p, in + (size_t)c * kSpillChunk + lo, cnt, stk + tid, dirs[w], opix[w],
+                                        mbox[w], hword + w);
         }
-        spill_close(p.sq.fill[p.round & 1], p.sq.ctr + p.round * kSpillCtrStride, cur);
-}
-
-template <bool kR64, bool kAny>
-__global__ __launch_bounds__(kSecBlock, VRT_SEC_WAVES_PER_EU) void k_secondary(SecondaryParams p)
-{
-        __shared__ uint2 stk[kStack * kSecBlock];
-        __shared__ float pts[VRT_SEC_WAVES][64][3];
-        __shared__ uint2 mbox[kAny && VRT_SEC_COOP ? VRT_SEC_WAVES : 1][64];
-        __shared__ unsigned long long hword[VRT_SEC_WAVES];
-        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-        const int64_t k = (int64_t)blockIdx.x * VRT_SEC_WAVES + wave;
-        SpillCursor cur;  // no compaction in the one-pixel-per-wave grid (p.sq.nchunks == 0)
-        cur.chunk = kSpillNone;
-        cur.fill = 0;
-        constexpr int mw = kAny && VRT_SEC_COOP ? 1 : 0;
-        secondary_pixel<kR64, kAny, kSecBlock>(p, k, lane, stk + tid, pts[wave], mbox[wave * mw], hword + wave,
-                                               cur);
 }
 
 // Persistent config 5: one resident generation of 4-wave workgroups; each
@@ -3113,9 +2759,6 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
 {
         __shared__ uint2 stk[kStack * kSecPBlock];
         __shared__ float pts[kSecPBlock / 64][64][3];
-        __shared__ uint2 mbox[kAny && VRT_SEC_COOP ? kSecPBlock / 64 : 1][64];
-        __shared__ unsigned long long hword[kSecPBlock / 64];
-        constexpr int mw = kAny && VRT_SEC_COOP ? 1 : 0;
         const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
         const int xcd = blockIdx.x & 7;
         SpillCursor cur;
@@ -3132,23 +2775,16 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
                                 break;
                         secondary_pixel<kR64, kAny, kSecPBlock>(
                                 p, (int64_t)slice_unit(p.units, x, (int)u, VRT_SEC_SLICE_CHUNK), lane, stk + tid,
-                                pts[wave], mbox[wave * mw], hword + wave, cur);
+                                pts[wave], cur);
                 }
         }
-        if (kAny && !VRT_SEC_COOP)
+        if (kAny)
                 spill_close(p.sq.fill[0], p.sq.ctr, cur);
 }
 
 #ifndef VRT_SEC_SPILL_T
 #define VRT_SEC_SPILL_T 12    // phase A stops below this many walking lanes (0: no compaction); round 4 with the streaming resume: 8 / 12 / 16 / 20 / 24 / 32 / 48 = 18.07 / 17.21 / 17.28 / 17.54 / 17.65 / 17.66 / 17.83 ms
 #endif
-#ifndef VRT_SEC_SPILL_T2
-#define VRT_SEC_SPILL_T2 24   // the same in resume rounds before the last
-#endif
-#ifndef VRT_SEC_ROUNDS
-#define VRT_SEC_ROUNDS 3      // resume launches
-#endif
-static_assert(VRT_SEC_ROUNDS >= 1 && VRT_SEC_ROUNDS < kSpillMaxRounds, "VRT_SEC_ROUNDS");
 static_assert(kSpillStack >= kStack, "SpillRec stack");
 
 SpillQueues spill_defaults()
@@ -3156,8 +2792,6 @@ SpillQueues spill_defaults()
         SpillQueues q;
         std::memset(&q, 0, sizeof q);
         q.t_first = VRT_SEC_SPILL_T;
-        q.t_next = VRT_SEC_SPILL_T2;
-        q.rounds = VRT_SEC_POOL_RESUME ? 1 : VRT_SEC_ROUNDS;  // the pooled round walks to the end
         q.stream = 0;  // set per launch (launch_secondary: films under 2^26 pixels)
         return q;
 }
@@ -3197,23 +2831,23 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
         const int64_t waves = mine * 64;
         if (waves == 0)
                 return hipGetLastError();
-#ifndef VRT_SEC_ANY
-#define VRT_SEC_ANY 1
-#endif
-        const bool any = VRT_SEC_ANY && !s_tri && !s_vox;
+        // no per-ray ids requested: the occlusion walk (+ compaction)
+        const bool any = !s_tri && !s_vox;
         const bool w = sp.sc.wide_leaves != 0;
-        if (q && secondary_uses_queue(rp.sc) && waves <= INT_MAX) {
+        if (!q || !secondary_uses_queue(rp.sc) || waves > INT_MAX)
+                return hipErrorInvalidValue;
+        {
                 sp.units = (int32_t)waves;
                 sp.q = *q;
                 const int cap = nranks > 1 ? std::max(8, rp.sc.sec_blocks - kCollectiveReserve) : rp.sc.sec_blocks;
                 const int g = (int)std::min<int64_t>(cap, ((waves + 3) / 4 + 7) & ~7LL);
                 void (*kern)(SecondaryParams) = w ? (any ? k_secondary_p<true, true> : k_secondary_p<true, false>)
                                                   : (any ? k_secondary_p<false, true> : k_secondary_p<false, false>);
-                const bool spill = !VRT_SEC_COOP && any && sq && sq->t_first > 0 && sq->nchunks > 0;
+                const bool spill = any && sq && sq->t_first > 0 && sq->nchunks > 0;
                 if (spill) {
                         sp.sq = *sq;
                         if (rp.test_flags & VRT_TEST_SPILL_ALL)  // test hook: stop at the first ray's end
-                                sp.sq.t_first = sp.sq.t_next = 64;
+                                sp.sq.t_first = 64;
                 }
                 hipLaunchKernelGGL(kern, dim3(g), dim3(kSecPBlock), 0, st, sp);
                 *q_waves = g * (kSecPBlock / 64);
@@ -3222,9 +2856,9 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                 if (hipError_t e = hipGetLastError())
                         return e;
                 if (spill) {
-                        // resume rounds: one resident generation each, every
-                        // wave taking 64 records at a time until the queue is
-                        // drained (an empty queue ends the launch at once)
+                        // the resume round: one resident generation walking
+                        // queue 0's records to their ends (an empty queue ends
+                        // the launch at once)
                         ResumeParams rp2;
                         std::memset(&rp2, 0, sizeof rp2);
                         rp2.sc = rp.sc;
@@ -3237,33 +2871,26 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                         rp2.test_flags = rp.test_flags;
                         rp2.W8 = rp.ntx * 8;
                         rp2.sq = sp.sq;
-                        rp2.sq.stream = (int64_t)rp.ntx * 8 * rp.nty * 8 < (1 << 26) ? 1 : 0;
+                        // the streaming round (films under 2^26 pixels: resume_stream packs the
+                        // pixel index in 26 bits; VRT_TEST_NO_STREAM takes the other path)
 #ifndef VRT_SEC_STREAM
 #define VRT_SEC_STREAM 1
 #endif
-                        rp2.sq.stream = VRT_SEC_POOL_RESUME && VRT_SEC_STREAM && rp2.sq.stream;
+                        rp2.sq.stream = VRT_SEC_STREAM && (int64_t)rp.ntx * 8 * rp.nty * 8 < (1 << 26) &&
+                                        !(rp.test_flags & VRT_TEST_NO_STREAM);
                         if (rp2.sq.stream) {
-                                rp2.round = 1;
                                 hipLaunchKernelGGL(w ? k_sec_stream<true> : k_sec_stream<false>, dim3(g),
                                                    dim3(kSecPBlock), 0, st, rp2);
                                 // the chunks the stream left (normally none): a small batch-pool launch
                                 hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(8),
                                                    dim3(kSecPBlock), 0, st, rp2);
                         } else {
-                                for (int r = 1; r <= sp.sq.rounds; ++r) {
-                                        rp2.round = r;
-                                        hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(g),
-                                                           dim3(kSecPBlock), 0, st, rp2);
-                                }
+                                hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(g),
+                                                   dim3(kSecPBlock), 0, st, rp2);
                         }
                 }
                 return hipGetLastError();
         }
-        void (*kern)(SecondaryParams) = w ? (any ? k_secondary<true, true> : k_secondary<true, false>)
-                                          : (any ? k_secondary<false, true> : k_secondary<false, false>);
-        hipLaunchKernelGGL(kern, dim3((unsigned)((waves + VRT_SEC_WAVES - 1) / VRT_SEC_WAVES)), dim3(kSecBlock), 0,
-                           st, sp);
-        return hipGetLastError();
 }
 
 // Rank-0 re-assembly of gathered per-rank tile buffers into the image.
@@ -3416,15 +3043,6 @@ bool render_uses_tail(const RenderParams &p)
 }
 bool render_budget_built() { return VRT_RENDER_BUDGET > 0; }
 
-#ifndef VRT_PERSIST
-#define VRT_PERSIST 1
-#endif
-#ifndef VRT_PERSIST_FAST
-#define VRT_PERSIST_FAST 1
-#endif
-#ifndef VRT_SEC_PERSIST
-#define VRT_SEC_PERSIST 1
-#endif
 // persistent waves for RefRec48 scenes without per-sample outputs;
 // large-leaf (RefRec64) scenes keep one-wave workgroups (-11 % persistent at
 // depth 6).  The fast-only kernel when the camera makes standard-range
@@ -3433,11 +3051,11 @@ bool render_budget_built() { return VRT_RENDER_BUDGET > 0; }
 RenderKind render_kind(const RenderParams &p, bool instrumented)
 {
         const SampleOut &so = p.so;
-        if (!VRT_PERSIST || instrumented || so.hit || so.tri || so.vox || so.rgb || so.cnt || p.sc.wide_leaves ||
+        if (instrumented || so.hit || so.tri || so.vox || so.rgb || so.cnt || p.sc.wide_leaves ||
             p.sc.persist_blocks <= 0)
                 return kRenderGrid;
         const CamParams &c = p.cam;
-        bool fast = VRT_PERSIST_FAST && p.sc.fast_ok && __builtin_bit_cast(uint32_t, c.tmin) == 0u &&
+        bool fast = p.sc.fast_ok && __builtin_bit_cast(uint32_t, c.tmin) == 0u &&
                     c.tmax == kFltMax;
         for (int k = 0; k < 3; ++k)
                 fast = fast && std::fabs(c.origin[k]) < 0x1p60f;
@@ -3556,7 +3174,7 @@ static int64_t camera_defer_count(const CamParams &c)
 
 bool secondary_uses_queue(const DevScene &sc)
 {
-        return VRT_SEC_PERSIST && sc.sec_blocks > 0;
+        return sc.sec_blocks > 0;
 }
 
 static int resident_blocks(const void *kern, int block, const hipDeviceProp_t &prop, hipError_t *e)
@@ -3626,6 +3244,7 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 const int g = std::min(cap, need);
                 if (kind == kRenderPersistFast) {
                         const bool tail = render_uses_tail(p);
+                        (void)tail;  // no budget built: never true
                         void (*kern)(RenderParams) = k_render_p<true>;
 #if VRT_RENDER_BUDGET > 0
                         if (tail)
@@ -3680,17 +3299,14 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 } else {
                         hipLaunchKernelGGL(k_render_p<false>, dim3(g), dim3(kPersistBlock), 0, st, p);
                 }
-                // failing adds per slice counter: every wave visits every
-                // slice (VRT_PERSIST_HELP), or only its own XCD's (g is a
-                // multiple of 8: g/8 blocks per XCD residue); with
-                // VRT_Q_PRECHECK the launch zeroes its counters itself (-1)
-                *q_waves = VRT_Q_PRECHECK ? -1 : (VRT_PERSIST_HELP ? g : g / 8) * (kPersistBlock / 64);
+                // failing adds per slice counter: every wave visits every slice
+                *q_waves = g * (kPersistBlock / 64);
                 for (int x = 0; x < 8; ++x)
                         slice_units[x] = slice_size(p.tiles_this_rank * 4, x, VRT_SLICE_CHUNK);
                 return hipGetLastError();
         }
         // round the grid up to a multiple of 8 (one slot per XCD)
-        const int grid = (p.tiles_this_rank * (4 / VRT_RENDER_WAVES) + 7) & ~7;
+        const int grid = (p.tiles_this_rank * (4) + 7) & ~7;
         void (*kern)(RenderParams) = instrumented ? (w ? k_render<true, true> : k_render<true, false>)
                                                   : (w ? k_render<false, true> : k_render<false, false>);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kRenderBlock), 0, st, p);
@@ -3806,7 +3422,7 @@ __device__ __forceinline__ f3 illum_dir(int i)
 // -43 %): the one-block-per-unit launch keeps the most rays in flight.
 __host__ __device__ __forceinline__ int trace_vblocks(int tiles)
 {
-        return (tiles * (4 / VRT_RENDER_WAVES) + 7) & ~7;
+        return (tiles * (4) + 7) & ~7;
 }
 
 // XCD-aware block order: block b of nb (a multiple of 8) -> its place in
@@ -3838,22 +3454,19 @@ __device__ __forceinline__ int chunk_place(int b, int nb)
 #ifndef VRT_PRIM_CHUNK
 #define VRT_PRIM_CHUNK 0
 #endif
-#ifndef VRT_CONES_CHUNK
-#define VRT_CONES_CHUNK 0
-#endif
 
 // 8x8-pixel tile of work unit u and this lane's pixel / sample.  Returns
 // false for padding units.
 __device__ __forceinline__ bool tile_lane_at(const RenderParams &p, int u, int tid, int &k, int &px, int &py,
                                              int &s, int &lx, int &ly)
 {
-        constexpr int kQ = 4 / VRT_RENDER_WAVES;  // work units per tile
+        constexpr int kQ = 4;  // work units per tile
         if (u >= p.tiles_this_rank * kQ)
                 return false;
         k = u / kQ;
         int tx, ty;
         deal_tile(tile_deal(p.ntx, p.nty, p.nranks), p.rank, k, tx, ty);
-        const int wave = (u % kQ) * VRT_RENDER_WAVES + (tid >> 6), lane = tid & 63;
+        const int wave = (u % kQ) + (tid >> 6), lane = tid & 63;
         s = lane & 3;
         const int pix = lane >> 2;
         lx = (wave & 1) * 4 + (pix & 3);
@@ -3923,7 +3536,7 @@ __device__ __forceinline__ void light_unit(const LightParams &p, uint2 *stk, int
         if (p.r.test_flags & VRT_TEST_LIGHT_TAIL)
                 m.deferred = true;  // test hook: every sample to k_light_tail
         else
-                ray_march_dispatch<false, kRenderBlock, 1, kR64, 0, VRT_LIGHT_BUDGET>(p.r.sc, r, stk + tid, nullptr,
+                ray_march_dispatch<false, kRenderBlock, 1, kR64, VRT_LIGHT_BUDGET>(p.r.sc, r, stk + tid, nullptr,
                                                                                      nullptr, m);
 #if VRT_LIGHT_DIAG
         {
@@ -4233,10 +3846,6 @@ __device__ __forceinline__ f3 cone_march_fast(const TraceParams &p, f3 o, f3 d)
         return diffuse;
 }
 
-#ifndef VRT_CONE_V
-#define VRT_CONE_V 4  // 1: cone_march_fast only; 2, 3: cone_march_axes without the cell / without the held il (A/B)
-#endif
-
 __device__ __forceinline__ int octant_of(const f3 &pt, const float4 &c)
 {
         return (pt.x > c.x ? 4 : 0) + (pt.y > c.y ? 2 : 0) + (pt.z > c.z ? 1 : 0);
@@ -4256,14 +3865,13 @@ __device__ __forceinline__ int octant_of(const f3 &pt, const float4 &c)
 // starts at +0 and under round-to-nearest never becomes -0, so the sums are
 // bit-identical.
 //
-// kCell: the descent also records the cell of the point it followed -- per
+// The descent also records the cell of the point it followed -- per
 // axis the half-open interval (lo, hi] cut by the centres whose octant
 // choice it used (pt > centre: lo, else hi; the octree's cells are nested,
 // max/min keep the tightest) -- and the next step at the same split level
 // whose point lies in that cell makes the same choices at every node of the
 // path, so it reuses the node (and whether the descent ended above the split
 // level) without descending.  Any other step descends from the root.
-template <int kCell>
 __device__ __forceinline__ f3 cone_march_axes(const TraceParams &p, f3 o, f3 d, const float co[6])
 {
         const float aperture = 0.577350269f, step = .1f, decay = 1.f;
@@ -4276,7 +3884,7 @@ __device__ __forceinline__ f3 cone_march_axes(const TraceParams &p, f3 o, f3 d, 
         f3 diffuse = mk3(0.f, 0.f, 0.f);
         int level = -1;
         float bound = 0.f;
-        // the last descent's cell (kCell)
+        // the last descent's cell
         f3 lo = mk3(0.f, 0.f, 0.f), hi = lo;
         int c_level = -1, c_split = 0;
         uint32_t c_ni = 0;
@@ -4298,39 +3906,33 @@ __device__ __forceinline__ f3 cone_march_axes(const TraceParams &p, f3 o, f3 d, 
                 int split = level;
                 uint32_t ni = 0;
                 bool same = false;
-                if (kCell && level == c_level && pt.x > lo.x && pt.x <= hi.x && pt.y > lo.y && pt.y <= hi.y &&
+                if (level == c_level && pt.x > lo.x && pt.x <= hi.x && pt.y > lo.y && pt.y <= hi.y &&
                     pt.z > lo.z && pt.z <= hi.z) {
                         split = c_split;
                         ni = c_ni;
-                        same = kCell >= 2;
+                        same = true;
                 } else {
                         uint32_t a = a0;
                         float4 c = c0;
                         int i = octant_of(pt, c0);
-                        if (kCell) {
-                                lo = mk3(-__builtin_inff(), -__builtin_inff(), -__builtin_inff());
-                                hi = mk3(__builtin_inff(), __builtin_inff(), __builtin_inff());
-                        }
+                        lo = mk3(-__builtin_inff(), -__builtin_inff(), -__builtin_inff());
+                        hi = mk3(__builtin_inff(), __builtin_inff(), __builtin_inff());
                         while (!(a & kLeafBit) && split) {
-                                if (kCell) {
-                                        if (i & 4) lo.x = std::max(lo.x, c.x); else hi.x = std::min(hi.x, c.x);
-                                        if (i & 2) lo.y = std::max(lo.y, c.y); else hi.y = std::min(hi.y, c.y);
-                                        if (i & 1) lo.z = std::max(lo.z, c.z); else hi.z = std::min(hi.z, c.z);
-                                }
+                                if (i & 4) lo.x = std::max(lo.x, c.x); else hi.x = std::min(hi.x, c.x);
+                                if (i & 2) lo.y = std::max(lo.y, c.y); else hi.y = std::min(hi.y, c.y);
+                                if (i & 1) lo.z = std::max(lo.z, c.z); else hi.z = std::min(hi.z, c.z);
                                 ni = a + (uint32_t)i;
                                 c = p.cc[ni];
                                 a = __float_as_uint(c.w);
                                 i = octant_of(pt, c);
                                 split--;
                         }
-                        if (kCell) {
-                                c_level = level;
-                                c_split = split;
-                                c_ni = ni;
-                        }
+                        c_level = level;
+                        c_split = split;
+                        c_ni = ni;
                 }
                 if (split == 0) {
-                        if (!same) {  // (kCell 2: the same node's cov and il are still held)
+                        if (!same) {  // (the same node's cov and il are still held)
                                 const LMRec *R = p.lm + ni;
                                 float L[9];
                                 cov = R->cov;
@@ -4376,7 +3978,6 @@ __device__ __forceinline__ f3 cone_march_ref(const TraceParams &p, f3 o, f3 d);
 __device__ __forceinline__ f3 cone_march(const TraceParams &p, f3 o, f3 d)
 {
         if (*p.lm_bad == 0u) {
-#if VRT_CONE_V >= 2
                 const f3 nd = -d;
                 float co[6];
 #pragma unroll
@@ -4385,9 +3986,8 @@ __device__ __forceinline__ f3 cone_march(const TraceParams &p, f3 o, f3 d)
                 const bool twin = (co[0] != 0.f && co[3] != 0.f) || (co[1] != 0.f && co[4] != 0.f) ||
                                   (co[2] != 0.f && co[5] != 0.f);
                 if (!twin)
-                        return cone_march_axes<VRT_CONE_V - 2>(p, o, d, co);
-#endif
-                return cone_march_fast(p, o, d);
+                        return cone_march_axes(p, o, d, co);
+                return cone_march_fast(p, o, d);  // a NaN direction
         }
         return cone_march_ref(p, o, d);
 }
@@ -4439,34 +4039,10 @@ __device__ __forceinline__ f3 cone_march_ref(const TraceParams &p, f3 o, f3 d)
 }
 
 // cone_trace(root, isect, min_voxel_size) with orthonormal_basis
-// (VRT/voxel_octree.cc:256-274, 313-330)
-__device__ __forceinline__ f3 cone_trace_isect(const TraceParams &p, f3 hit, f3 n)
-{
-        const float hx[6] = { 0.000000f, 0.000000f, 0.823639f, 0.509037f, -0.509037f, -0.823639f };
-        const float hy[6] = { 0.000000f, 0.866025f, 0.267617f, -0.700629f, -0.700629f, 0.267617f };
-        const float hz[6] = { 1.0f, 0.5f, 0.5f, 0.5f, 0.5f, 0.5f };
-        const float hw[6] = { 0.25f, 0.15f, 0.15f, 0.15f, 0.15f, 0.15f };
-        const float sg = (0.0f > n.z) ? -1.0f : 1.0f;
-        const float a0 = -1.0f / (sg + n.z);
-        const float a1 = n.x * n.y * a0;
-        const f3 t = mk3(1.0f + sg * n.x * n.x * a0, sg * a1, -sg * n.x);
-        const f3 bb = mk3(a1, sg + n.y * n.y * a0, -n.y);
-        f3 diffuse = mk3(0.f, 0.f, 0.f);
-        for (int i = 0; i < 6; ++i) {
-                f3 r = mk3(0.f, 0.f, 0.f);
-                r = r + t * hx[i];
-                r = r + bb * hy[i];
-                r = r + n * hz[i];
-                const f3 cd = normalize(r);
-                const f3 cm = cone_march(p, hit, cd);
-                diffuse = diffuse + cm * hw[i];
-        }
-        return diffuse;
-}
-
-// cone_trace_isect over a sample record (hit point in rec[0].xyz, normal in
-// rec[1].xyz): the same operations in the same order, the record re-read per
-// cone (volatile asm keeps the compiler from hoisting it across the marches)
+// (VRT/voxel_octree.cc:256-274, 313-330) over a sample record (hit point in
+// rec[0].xyz, normal in rec[1].xyz), the record re-read and the basis remade
+// per cone -- the same operations, so the same values (volatile asm keeps the
+// compiler from hoisting the record across the marches)
 __device__ __forceinline__ f3 cone_trace_rec(const TraceParams &p, const float4 *rec)
 {
         const float hx[6] = { 0.000000f, 0.000000f, 0.823639f, 0.509037f, -0.509037f, -0.823639f };
@@ -4495,63 +4071,6 @@ __device__ __forceinline__ f3 cone_trace_rec(const TraceParams &p, const float4 
         return diffuse;
 }
 
-// trace(root, ray, 5, true) per sample + Film::add(c * .25f)
-// (VRT/main.cc:10-30, 118-123)
-template <bool kR64>
-__global__ __launch_bounds__(kRenderBlock) void k_trace(TraceParams p)
-{
-        __shared__ uint2 stk[kStack * kRenderBlock];
-        const int tid = threadIdx.x, lane = tid & 63;
-        const int u = chunk_place<VRT_CONES_CHUNK>(blockIdx.x, gridDim.x);
-        int k, px, py, s, lx, ly;
-        if (!tile_lane(p.r, u, k, px, py, s, lx, ly))
-                return;
-        const CamParams &c = p.r.cam;
-        const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py,
-                                 sample_x(s), sample_y(s));
-        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]),
-                                 dn, c.tmin, c.tmax);
-        MarchResult m;
-        ray_march_dispatch<false, kRenderBlock, true, kR64>(p.r.sc, r, stk + tid, nullptr, nullptr, m);
-        f3 col;
-        if (m.hit) {
-                f3 nrm;
-                const f3 albedo = hit_albedo(p.r.sc, m, nrm);
-                const f3 indirect = cone_trace_isect(p, m.hp, nrm);
-                const f3 direct = compute_illum(p.lm, m.node, -r.d);
-                const f3 l = indirect + direct;
-                col = mk3(albedo.x * l.x, albedo.y * l.y, albedo.z * l.z);
-        } else {
-                col = sky(r.d.y);
-        }
-        const size_t si = ((size_t)py * c.nx + px) * 4 + s;
-        if (p.r.so.hit) p.r.so.hit[si] = m.hit ? 1 : 0;
-        if (p.r.so.rgb) {
-                p.r.so.rgb[3 * si + 0] = col.x;
-                p.r.so.rgb[3 * si + 1] = col.y;
-                p.r.so.rgb[3 * si + 2] = col.z;
-        }
-        const f3 cq = col * .25f;
-        const int l0 = lane & ~3;
-        float acc[3] = { 0.0f, 0.0f, 0.0f };
-        const float cv[3] = { cq.x, cq.y, cq.z };
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                        acc[q] += __shfl(cv[q], l0 + j, 64);
-        }
-        if (s == 0) {
-                float *o;
-                if (p.r.image_layout)
-                        o = p.r.out + ((size_t)py * c.nx + px) * 3;
-                else
-                        o = p.r.out + ((size_t)k * 64 + ly * 8 + lx) * 3;
-                o[0] = acc[0];
-                o[1] = acc[1];
-                o[2] = acc[2];
-        }
-}
 
 // ---- split trace: primary pass, one lane per (sample, cone), film add ----
 // Primary pass: trace()'s ray_march + get_albedo + leaf compute_illum(-d);
@@ -4608,7 +4127,7 @@ __device__ __forceinline__ void trace_prim_unit(const TraceParams &p, uint2 *stk
         if (p.r.test_flags & VRT_TEST_PRIM_TAIL)
                 m.deferred = true;  // test hook: every sample to k_trace_prim_tail
         else
-                ray_march_dispatch<false, kRenderBlock, 1, kR64, 0, VRT_PRIM_BUDGET>(p.r.sc, r, stk + tid, nullptr,
+                ray_march_dispatch<false, kRenderBlock, 1, kR64, VRT_PRIM_BUDGET>(p.r.sc, r, stk + tid, nullptr,
                                                                                     nullptr, m);
         if (m.deferred) {
                 const uint32_t j = atomicAdd(p.tail_n, 1u);
@@ -4669,26 +4188,17 @@ __global__ __launch_bounds__(64) void k_trace_prim_tail(TraceParams p)
 __global__ __launch_bounds__(64, VRT_CONES_WAVES_PER_EU) void k_cones_film(TraceParams p)
 {
         const int u = blockIdx.x;
-        constexpr int kQ = 4 / VRT_RENDER_WAVES;
+        constexpr int kQ = 4;
         if (u >= p.r.tiles_this_rank * kQ)
                 return;
         const int64_t slot = (int64_t)u * 64 + threadIdx.x;
-#ifndef VRT_CONES_RELOAD
-#define VRT_CONES_RELOAD 1
-#endif
         f3 col;
         if (p.rec[4 * slot + 0].w != 0.f) {
-                f3 diffuse;
-                if (VRT_CONES_RELOAD) {
-                        // cone_trace_isect with the hit point and normal read
-                        // from the sample record per cone (L2 hits) and the
-                        // basis remade per cone -- the same values -- rather
-                        // than held in registers across the 6 cone marches
-                        diffuse = cone_trace_rec(p, p.rec + 4 * slot);
-                } else {
-                        const float4 r0 = p.rec[4 * slot + 0], r1 = p.rec[4 * slot + 1];
-                        diffuse = cone_trace_isect(p, mk3(r0.x, r0.y, r0.z), mk3(r1.x, r1.y, r1.z));
-                }
+                // cone_trace with the hit point and normal read from the
+                // sample record per cone (L2 hits) and the basis remade per
+                // cone -- the same values -- rather than held in registers
+                // across the 6 cone marches
+                const f3 diffuse = cone_trace_rec(p, p.rec + 4 * slot);
                 const float4 r2 = p.rec[4 * slot + 2], r3 = p.rec[4 * slot + 3];
                 const f3 direct = compute_illum(p.lm, __float_as_uint(r3.x), mk3(r3.y, r3.z, r3.w));
                 const f3 lsum = diffuse + direct;
@@ -4798,11 +4308,6 @@ hipError_t launch_trace(const TraceParams &p, hipStream_t st)
 {
         if (p.r.tiles_this_rank <= 0)
                 return hipSuccess;
-        const int grid = trace_vblocks(p.r.tiles_this_rank);
-        if (!p.rec) {
-                hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace<true> : k_trace<false>, dim3(grid), dim3(kRenderBlock), 0, st, p);
-                return hipGetLastError();
-        }
         if (hipError_t e = launch_trace_prim(p, st))
                 return e;
         return launch_cones(p, st);
@@ -4855,13 +4360,10 @@ bool build_flag(const char *name, int64_t *value)
         } kFlags[] = {
                 { "VRT_SEC_SPILL_T", VRT_SEC_SPILL_T },
                 { "VRT_SEC_STREAM", VRT_SEC_STREAM },
-                { "VRT_SEC_ANY", VRT_SEC_ANY },
-                { "VRT_SEC_PERSIST", VRT_SEC_PERSIST },
+
                 { "VRT_SEC_SLICE_CHUNK", VRT_SEC_SLICE_CHUNK },
-                { "VRT_PERSIST", VRT_PERSIST },
-                { "VRT_PERSIST_FAST", VRT_PERSIST_FAST },
+
                 { "VRT_SLICE_CHUNK", VRT_SLICE_CHUNK },
-                { "VRT_NODE_BOX", VRT_NODE_BOX },
                 { "VRT_DEAL_BLOCK", VRT_DEAL_BLOCK },
                 { "VRT_DEAL_WEIGHT", VRT_DEAL_WEIGHT },
                 { "VRT_LIGHT_BUDGET", VRT_LIGHT_BUDGET },
