@@ -646,7 +646,10 @@ def main():
     img_shape = (a.height, a.width) if secondary else (a.height, a.width, 3)
     imgs = [torch.zeros(img_shape, dtype=torch.float32, device=dev) for _ in range(nfl)]
     img = imgs[0]
-    nbuf = max(2, nfl)  # multi-rank buffers: one per frame in flight (>= 2: gather k overlaps frame k+1)
+    # multi-rank buffers: two per frame in flight, so the render that reuses
+    # frame k's buffer (frame k + nbuf, on frame k's stream) finds frame k's
+    # collective long finished instead of waiting for it
+    nbuf = max(2, 2 * nfl)
     if secondary:
         # config 5: rays per frame are data dependent (64 per primary hit):
         # count them per pose once, outside the timed region
@@ -664,6 +667,12 @@ def main():
         # in-place views (a rehearsal's 1-rank group gathers into row 0 only)
         gl = [list(g[:world].unbind(0)) for g in gathered] if rank == 0 else [None] * nbuf
     works = [None] * nbuf
+    # a frame's collective completion (and on rank 0 its re-assembly) is
+    # tracked on a side stream, never on the render streams: a render waits
+    # only for the collective that last read the buffer it reuses (buf_free)
+    post = torch.cuda.Stream(dev)
+    buf_free = [torch.cuda.Event() for _ in range(nbuf)]
+    buf_used = [False] * nbuf
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(a.steps)]
     # N-rank diagnostics on every DIAG_EVERY-th timed frame (each event record
@@ -681,10 +690,12 @@ def main():
         """frame k's stream slot and buffer slot"""
         return k % nfl, k % nbuf
 
-    def finish(b, s):
-        """Rank 0: re-assemble the frame gathered into buffer b, on stream s."""
+    def finish(b):
+        """Buffer b's collective complete on the side stream; rank 0 then
+        re-assembles the frame there; buf_free[b] marks the buffer free."""
         if works[b] is None:
             return
+        s = post
         with torch.cuda.stream(s):
             works[b].wait()  # stream-wait on the collective, no host block
         works[b] = None
@@ -693,9 +704,8 @@ def main():
         if k is not None:
             ev_coll[k].record(s)
             coll_done.append(k)
-        # rank 0 re-assembles (each buffer slot into its own image: frames in
-        # flight); a rehearsal of rank r >= 1's share does what that rank
-        # does -- render + gather send, no unpack
+        # rank 0 re-assembles; a rehearsal of rank r >= 1's share does what
+        # that rank does -- render + gather send, no unpack
         if rank == 0 and not (rehearse and cur["share"] != 0):
             if k is not None:
                 ev_unp[k][0].record(s)
@@ -708,6 +718,15 @@ def main():
             if k is not None:
                 ev_unp[k][1].record(s)
                 unp_done.append(k)
+        buf_free[b].record(s)
+        buf_used[b] = True
+
+    def reuse(b, s):
+        """Before a frame renders into buffer b on stream s: the collective
+        (and unpack) of the frame that used b last have finished."""
+        finish(b)  # normally done already
+        if buf_used[b]:
+            s.wait_event(buf_free[b])
 
     def step_secondary(k, timed):
         cam = cams[k % a.poses]
@@ -721,7 +740,7 @@ def main():
             if timed:
                 ev[k][1].record(s)
             return
-        finish(b, s)  # frame k - nbuf used these buffers (normally finished already)
+        reuse(b, s)  # frame k - nbuf used these buffers
         if rank == 0:
             with torch.cuda.stream(s):
                 visb[b].zero_()  # the previous reduce summed into rank 0's buffer
@@ -735,8 +754,7 @@ def main():
             with torch.cuda.stream(s):
                 works[b] = dist.reduce(visb[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
             frame_of[b] = k if (timed and k % DIAG_EVERY == 0) else None
-            jp, bp = sl(k - 1)
-            finish(bp, streams[jp])  # frame k-1: its reduce overlapped this render
+            finish(sl(k - 1)[1])  # frame k-1: its reduce overlapped this render
         else:
             host = visb[b].cpu()
             dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
@@ -764,7 +782,7 @@ def main():
             if timed:
                 ev[k][1].record(s)
             return
-        finish(b, s)  # frame k - nbuf used this buffer pair (normally finished already)
+        reuse(b, s)  # frame k - nbuf used this buffer pair
         render(cam, cur["share"], nshare, 0, tiles[b].data_ptr(), s)
         if timed:
             ev[k][1].record(s)
@@ -777,8 +795,7 @@ def main():
             with torch.cuda.stream(s):
                 works[b] = dist.gather(tiles[b], gl[b], dst=0, async_op=True)
             frame_of[b] = k if (timed and k % DIAG_EVERY == 0) else None
-            jp, bp = sl(k - 1)
-            finish(bp, streams[jp])  # frame k-1: its gather overlapped this render
+            finish(sl(k - 1)[1])  # frame k-1: its gather overlapped this render
         else:  # gloo rehearsal (several ranks on one GPU): host-staged gather
             host = tiles[b].cpu()
             hl = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
@@ -789,7 +806,7 @@ def main():
 
     def drain():
         for b in range(nbuf):
-            finish(b, stream)
+            finish(b)
 
     def timed_run():
         """W warm-up steps, then K timed steps between barrier + synchronize

@@ -373,7 +373,7 @@ struct vrt_scene {
         hipEvent_t spill_ev[2] = {};
         bool spill_live[2] = {};
         hipStream_t spill_stream[2] = {};  // the set's last user (a stream keeps its set)
-        uint32_t *h_spill = nullptr;       // pinned: per set, chunks phase A took in its last launch
+        uint32_t *h_spill = nullptr;       // pinned: per set, its last launch's round counters (ctr[0..7])
         uint32_t spill_want = 0;           // queue-0 chunks the next launch sizes for (0: first estimate)
         int spill_next = 0;
         int spill_last = -1;  // the set the last config-5 launch compacted with (vrt_secondary_spill_counts)
@@ -387,10 +387,6 @@ struct vrt_scene {
         // of kQueueSlots counter sets, each with its bases and the event of
         // its last launch
         uint32_t *d_queue = nullptr;
-        // budgeted render (render_uses_tail): per queue slot, the list of
-        // pixels left to k_render_tail (rtail_words words each)
-        uint32_t *d_rtail = nullptr;
-        size_t rtail_words = 0;
         uint32_t q_base[kQueueSlots][8] = {};
         hipEvent_t q_ev[kQueueSlots] = {};
         bool q_live[kQueueSlots] = {};
@@ -1031,8 +1027,6 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                                 (void)hipEventSynchronize(s->spill_ev[k]);
                 if (s->d_mem)
                         (void)hipFree(s->d_mem);
-                if (s->d_rtail)
-                        (void)hipFree(s->d_rtail);
                 for (TraceSet &t : s->ts) {
                         if (t.lm)
                                 (void)hipFree(t.lm);
@@ -1289,34 +1283,9 @@ static int queue_release(vrt_scene *s, int slot, hipStream_t st, const int slice
 static void queue_reset(vrt_scene *s, int slot, hipStream_t st)
 {
         (void)hipMemsetAsync(s->d_queue + (size_t)slot * kQueueWords, 0, kQueueBytes, st);
-        if (s->d_rtail)  // the budgeted render's list count and done word
-                (void)hipMemsetAsync(s->d_rtail + (size_t)slot * s->rtail_words, 0, kRenderTailList * 4, st);
         std::memset(s->q_base[slot], 0, sizeof s->q_base[slot]);
         if (hipEventRecord(s->q_ev[slot], st) == hipSuccess)
                 s->q_live[slot] = true;
-}
-
-// The budgeted render's left-pixel list of queue slot `slot`, grown to this
-// launch's pixels (budget builds only; caller holds s->mu).
-static int rtail_setup(vrt_scene *s, RenderParams &p, int slot)
-{
-        p.rtail = nullptr;
-        if (!render_budget_built() || slot < 0)
-                return VRT_OK;
-        const size_t words = kRenderTailList + (size_t)p.tiles_this_rank * 64;
-        if (s->rtail_words < words) {
-                if (s->d_rtail) {
-                        HIPCHK(hipDeviceSynchronize());  // launches on any stream may use the lists
-                        (void)hipFree(s->d_rtail);
-                        s->d_rtail = nullptr;
-                        s->rtail_words = 0;
-                }
-                HIPCHK(hipMalloc(&s->d_rtail, words * 4 * kQueueSlots));
-                HIPCHK(hipMemset(s->d_rtail, 0, words * 4 * kQueueSlots));
-                s->rtail_words = words;
-        }
-        p.rtail = s->d_rtail + (size_t)slot * s->rtail_words;
-        return VRT_OK;
 }
 
 // One render launch on stream st (caller holds s->mu).
@@ -1326,8 +1295,6 @@ static int render_launch(vrt_scene *s, RenderParams &p, bool instrumented, hipSt
         (void)hipGetLastError();  // a leftover error of an earlier call is not this launch's
         if (render_kind(p, instrumented) != kRenderGrid) {
                 if (int rc = queue_take(s, st, &p.q, &slot))
-                        return rc;
-                if (int rc = rtail_setup(s, p, slot))
                         return rc;
         }
         int waves = 0, units[8];
@@ -1346,12 +1313,13 @@ static int ts_acquire(vrt_scene *s, int i, hipStream_t st);
 static int ts_release(vrt_scene *s, int i, hipStream_t st);
 
 // Compaction queue of one config-5 launch (SpillQueues).  Its
-// size is an estimate: a full queue only means the rays beyond it finish in
-// their first wave (spill_reserve returns no threshold), so any size gives
-// the same images.  The first launch sizes queue 0 for 1/32 of the rank's
-// secondary rays (1080p: 4.1 M records, 0.5 GiB); after every launch the
-// chunks phase A took are copied to pinned memory, and a later launch sizes
-// for 1.5 x that (x 2 after an overflow), growing, never shrinking.  Only
+// size is an estimate: when the queue is full, the rays that stop finish
+// their walks in place (spill_room), so any size gives the same images.  The
+// first launch sizes queue 0 for 1/32 of the rank's secondary rays (1080p:
+// 4.1 M records, 0.5 GiB) plus one partly filled chunk per resident wave;
+// after every launch its counters are copied to pinned memory, and a later
+// launch sizes for 1.25 x the records its phase A stopped (queued + finished
+// in place), growing, never shrinking.  Only
 // queue 0's records are allocated: the one pooled resume round walks every
 // saved ray to its end (queue 1's fill words list the streaming round's
 // leftover chunks).  The scene keeps two sets; a stream keeps using the set
@@ -1359,7 +1327,7 @@ static int ts_release(vrt_scene *s, int i, hipStream_t st);
 // (frames in flight on two streams), waiting for its last user's event.
 // sq->nchunks stays 0 (no compaction) when the build disables it or the
 // allocation fails.
-constexpr uint32_t kSpillCapMax = 1u << 24;  // chunks: 2 GiB of records at most
+constexpr uint32_t kSpillCapMax = (1u << 24) / kSpillChunk;  // chunks: 2 GiB of records at most
 static int spill_setup(vrt_scene *s, int64_t rays, hipStream_t st, SpillQueues *sq, int *set)
 {
         *sq = spill_defaults();
@@ -1383,16 +1351,16 @@ static int spill_setup(vrt_scene *s, int64_t rays, hipStream_t st, SpillQueues *
         if (!s->spill_ev[k])
                 HIPCHK(hipEventCreateWithFlags(&s->spill_ev[k], hipEventDisableTiming));
         if (!s->h_spill) {
-                HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&s->h_spill), 2 * sizeof(uint32_t),
+                HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&s->h_spill), 16 * sizeof(uint32_t),
                                      hipHostMallocDefault));
-                s->h_spill[0] = s->h_spill[1] = 0;
+                std::memset(s->h_spill, 0, 16 * sizeof(uint32_t));
         }
-        // what the finished launches of either set took
+        // what the finished launches of either set stopped: records queued
+        // (ctr[2]) + records finished in place for want of room (ctr[5])
         for (int i = 0; i < 2; ++i)
                 if (s->spill_live[i] && s->spill_cap[i] && hipEventQuery(s->spill_ev[i]) == hipSuccess) {
-                        const uint32_t took = s->h_spill[i];
-                        const uint64_t w = took >= s->spill_cap[i] ? 2ull * s->spill_cap[i]  // overflowed
-                                                                    : (3ull * took + 1) / 2;
+                        const uint64_t need = (uint64_t)s->h_spill[8 * i + 2] + s->h_spill[8 * i + 5];
+                        const uint64_t w = (need * 5 / 4 + kSpillChunk - 1) / kSpillChunk;
                         s->spill_want = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(s->spill_want, w), kSpillCapMax);
                 }
         if (s->spill_live[k] && s->spill_stream[k] != st)
@@ -1432,12 +1400,12 @@ static int spill_setup(vrt_scene *s, int64_t rays, hipStream_t st, SpillQueues *
         return VRT_OK;
 }
 
-// After a config-5 launch with compaction set k on st: its phase-A chunk
-// count to pinned memory (spill_setup reads it once the set's event has
-// passed) and the set's event.
+// After a config-5 launch with compaction set k on st: its counters to
+// pinned memory (spill_setup reads them once the set's event has passed) and
+// the set's event.
 static int spill_done(vrt_scene *s, int k, const SpillQueues &sq, hipStream_t st)
 {
-        HIPCHK(hipMemcpyAsync(s->h_spill + k, sq.ctr, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(s->h_spill + 8 * k, sq.ctr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipEventRecord(s->spill_ev[k], st));
         s->spill_live[k] = true;
         s->spill_stream[k] = st;
@@ -1855,7 +1823,7 @@ extern "C" int vrt_scene_scratch_bytes(vrt_scene *s, int64_t *bytes, int64_t *sp
                         sp += (int64_t)kSpillMaxRounds * kSpillCtrStride * 4 + 2 * fb +
                               (int64_t)s->spill_cap[k] * kSpillChunk * (int64_t)sizeof(SpillRec);
                 }
-        int64_t t = sp + (int64_t)s->light_bytes + (int64_t)s->rtail_words * 4 * kQueueSlots + (int64_t)s->ho.bytes;
+        int64_t t = sp + (int64_t)s->light_bytes + (int64_t)s->ho.bytes;
         for (const TraceSet &ts : s->ts) {
                 if (ts.lm)
                         t += (int64_t)s->nodes.size() * (int64_t)(sizeof(LMRec) + sizeof(float4)) + 256;

@@ -394,11 +394,7 @@ struct RenderParams {
         float *out;
         SampleOut so;
         WorkQueue q;           // persistent launches only
-        uint32_t *rtail;       // budgeted render (render_uses_tail): [0] count of left pixels, [kRenderTailDone]
-                               // the tail kernel's done count, from [kRenderTailList] unit << 4 | pixel
 };
-constexpr int kRenderTailDone = 32;
-constexpr int kRenderTailList = 64;
 
 // ---- full trace() -------------------------------------
 // Per-node cone-tracing state (80 B): VoxelOctree::coverage and illum[6]
@@ -484,9 +480,6 @@ int test_flags();
 // persistent kinds take their units from p.q.
 enum RenderKind { kRenderGrid = 0, kRenderPersist = 1, kRenderPersistFast = 2 };
 RenderKind render_kind(const RenderParams &p, bool instrumented);
-// the launch is budgeted and needs p.rtail (VRT_RENDER_BUDGET builds)
-bool render_uses_tail(const RenderParams &p);
-bool render_budget_built();
 // upper bound on the camera rays of the film that fail the fast-only
 // kernel's per-wave check (vrt_kernels.hip; cached for the last 32 cameras)
 int64_t camera_defer_bound(const CamParams &c);

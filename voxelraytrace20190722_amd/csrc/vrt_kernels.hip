@@ -1583,22 +1583,34 @@ __device__ __forceinline__ void spill_close(uint32_t *fills, uint32_t *ctr, cons
         atomicAdd(ctr + 2, lane == 0 ? c.fill : 0u);
 }
 
-// Before a group of up to 64 rays (every lane active, wave-uniform): room
-// for 64 more records in the cursor's chunk, taking the queue's next chunk
-// if needed.  Returns the stop threshold the group may use: t, or 0 (no
-// compaction, or the queue is full).
-__device__ __forceinline__ uint32_t spill_reserve(const SpillQueues &q, uint32_t *ctr, uint32_t *fills,
-                                                  SpillCursor &c, uint32_t t)
+// The stop threshold a group of rays may use: t, or 0 (no compaction, or
+// the queue was found full).
+__device__ __forceinline__ uint32_t spill_threshold(const SpillQueues &q, const SpillCursor &c, uint32_t t)
 {
-        if (q.nchunks == 0 || t == 0 || c.chunk == kSpillFull)
-                return 0u;
-        if (c.chunk != kSpillNone && c.fill + 64u <= kSpillChunk)
-                return t;
-        spill_close(fills, ctr, c);
-        const uint32_t k = take_n(ctr, 1u);
-        c.chunk = k < q.nchunks ? k : kSpillFull;
-        c.fill = 0;
-        return c.chunk == kSpillFull ? 0u : t;
+        return (q.nchunks == 0 || t == 0 || c.chunk == kSpillFull) ? 0u : t;
+}
+
+// After a group's walks, n > 0 of its rays stopped (every lane active,
+// wave-uniform): room for n more records in the cursor's chunk, taking the
+// queue's next chunk when they do not fit -- so chunks fill up whatever the
+// group sizes.  false: the queue is full (the caller finishes those rays in
+// place); their count goes to ctr[5] (the host sizes the next frame's queue
+// from ctr[2] + ctr[5]).
+__device__ __forceinline__ bool spill_room(const SpillQueues &q, uint32_t *ctr, uint32_t *fills, SpillCursor &c,
+                                           uint32_t n)
+{
+        if (c.chunk != kSpillFull && c.chunk != kSpillNone && c.fill + n <= kSpillChunk)
+                return true;
+        if (c.chunk != kSpillFull) {
+                spill_close(fills, ctr, c);
+                const uint32_t k = take_n(ctr, 1u);
+                c.chunk = k < q.nchunks ? k : kSpillFull;
+                c.fill = 0;
+        }
+        if (c.chunk != kSpillFull)
+                return true;
+        take_n(ctr + 5, n);
+        return false;
 }
 
 // The stopped rays of a group (`spilled`, after the walks): each writes its
@@ -1686,7 +1698,7 @@ constexpr int kRenderBlock = 64;
 // standard-range instantiation is compiled in (fewer live registers); a wave
 // whose rays need another path returns false before writing anything and the
 // caller defers the unit to k_render_defer.
-template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false, int kBudget = 0>
+template <bool kCount, bool kR64, int kS, bool kSamples = true, bool kFastOnly = false>
 __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wave, int lane, uint2 *stk,
                                             uint32_t *stk_aux, uint32_t *path_rem)
 {
@@ -1745,7 +1757,7 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         if (kFastOnly) {
                 if (!wave_fast_std(p.sc, r) || (p.test_flags & VRT_TEST_FORCE_DEFER))
                         return false;
-                ray_march<false, true, kS, kFastStd, true, kR64, kBudget>(p.sc, r, stk, nullptr, nullptr, m);
+                ray_march<false, true, kS, kFastStd, true, kR64>(p.sc, r, stk, nullptr, nullptr, m);
         } else {
                 ray_march_dispatch<kCount, kS, true, kR64>(p.sc, r, stk, stk_aux, path_rem, m);
         }
@@ -1763,17 +1775,8 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         if (!kSamples)
                 (void)sample_of(lane_now(), px, py, s, lx, ly);
 
-        // kBudget: a pixel with a sample whose walk hit the budget is left to
-        // k_render_tail (all 4 samples re-walked there, 8 lanes per ray)
-        bool pdef = false;
-        if (kBudget) {
-                const uint64_t dm = __ballot(m.deferred);
-                pdef = dm != 0 && ((dm >> (lane_now() & ~3)) & 0xFull) != 0;
-        }
         f3 col;
-        if (pdef) {
-                col = mk3(0.f, 0.f, 0.f);
-        } else if (m.hit) {
+        if (m.hit) {
                 f3 nrm;
                 RayK rs;  // shade_hit reads the direction only
                 rs.d = dn;
@@ -1813,10 +1816,7 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                 for (int q = 0; q < 3; ++q)  // lane l0 + j's value (a wave64 permute by our own lane id)
                         acc[q] += __int_as_float(__builtin_amdgcn_ds_bpermute((l0 + j) << 2, __float_as_int(cv[q])));
         }
-        if (kBudget && s == 0 && pdef) {
-                const uint32_t j = atomicAdd(p.rtail, 1u);  // the deferring lanes' adds: one atomic per wave
-                p.rtail[kRenderTailList + j] = (uint32_t)(k * 4 + wave) << 4 | (uint32_t)(lane >> 2);
-        } else if (s == 0) {
+        if (s == 0) {
                 float *o;
                 if (p.image_layout)
                         o = p.out + ((size_t)py * c.nx + px) * 3;
@@ -1901,7 +1901,7 @@ constexpr int kCollectiveReserve = 32;
 #ifndef VRT_PERSIST_WAVES_PER_EU
 #define VRT_PERSIST_WAVES_PER_EU 6
 #endif
-template <bool kFastOnly, int kBudget = 0>
+template <bool kFastOnly>
 __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_render_p(RenderParams p)
 {
         __shared__ uint2 stk[kStack * kPersistBlock];
@@ -1923,7 +1923,7 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
 #if VRT_UNIT_DIAG
                         const uint32_t dg_u0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly, kBudget>(
+                        const bool done = render_unit<false, false, kPersistBlock, false, kFastOnly>(
                                 p, kq >> 2, kq & 3, lane, stk + tid, nullptr, nullptr);
 #if VRT_UNIT_DIAG
                         {
@@ -2008,77 +2008,6 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
                         p.q.defer[x * kQueueStride + kDeferTake] = 0u;
                 }
                 p.q.defer[kDeferDoneWord] = 0u;
-        }
-}
-
-// The pixels k_render_p<true, kBudget> left (a sample's walk reached the
-// triangle-test budget): each of a pixel's 4 gen_rays4 samples re-walked
-// from the root by a group of 8 lanes on that one ray (leaf_isect_grp: the
-// leaf's records split over the group, ray_march_isect's first minimum
-// kept), 2 pixels per wave; shading, and Film::add of the 4 samples in order
-// -- the values the unbudgeted walk writes.  The last wave zeroes the list's
-// count for the queue slot's next launch.
-template <bool kR64>
-__global__ __launch_bounds__(64) void k_render_tail(RenderParams p)
-{
-        constexpr int kG = 8;
-        __shared__ uint2 stk[kStack * 64];
-        const uint32_t n = __builtin_amdgcn_readfirstlane(p.rtail[0]);
-        const int lane = threadIdx.x, half = lane >> 5, s = (lane >> 3) & 3;
-        const CamParams &c = p.cam;
-        for (uint32_t i0 = blockIdx.x * 2; i0 < n; i0 += gridDim.x * 2) {
-                const uint32_t i = i0 + (uint32_t)half;
-                int px = 0, py = 0, k = 0, lx = 0, ly = 0;
-                f3 cq = mk3(0.f, 0.f, 0.f);
-                if (i < n) {  // whole groups: both halves' lanes alike
-                        const uint32_t e = p.rtail[kRenderTailList + i];
-                        const int kq = (int)(e >> 4), pix = (int)(e & 15u), wave = kq & 3;
-                        k = kq >> 2;
-                        int tx, ty;
-                        deal_tile(tile_deal(p.ntx, p.nty, p.nranks), p.rank, k, tx, ty);
-                        lx = (wave & 1) * 4 + (pix & 3);
-                        ly = (wave >> 1) * 4 + (pix >> 2);
-                        px = tx * 8 + lx;
-                        py = (ty + p.ty0) * 8 + ly;
-                        const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py, sample_x(s),
-                                                 sample_y(s));
-                        const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]), dn, c.tmin, c.tmax);
-                        MarchResult m;
-                        ray_march_dispatch<false, 64, kG, kR64>(p.sc, r, stk + lane, nullptr, nullptr, m);
-                        f3 col;
-                        if (m.hit) {
-                                f3 nrm;
-                                col = shade_hit(p.sc, r, m, nrm);
-                        } else {
-                                col = sky(dn.y);
-                        }
-                        cq = col * .25f;
-                }
-                // Film::add of samples 0..3 (lanes half*32 + 8j) in order, from zero
-                const int l0 = lane & 32;
-                float acc[3] = { 0.0f, 0.0f, 0.0f };
-                const float cv[3] = { cq.x, cq.y, cq.z };
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                        for (int q = 0; q < 3; ++q)
-                                acc[q] += __int_as_float(
-                                        __builtin_amdgcn_ds_bpermute((l0 + 8 * j) << 2, __float_as_int(cv[q])));
-                }
-                if (i < n && (lane & 31) == 0) {
-                        float *o = p.image_layout ? p.out + ((size_t)py * c.nx + px) * 3
-                                                  : p.out + ((size_t)k * 64 + ly * 8 + lx) * 3;
-                        o[0] = acc[0];
-                        o[1] = acc[1];
-                        o[2] = acc[2];
-                }
-        }
-        // every wave has read the count: the last one zeroes it (and the done
-        // word) for the slot's next launch
-        const uint32_t fin = take_unit(p.rtail + kRenderTailDone);
-        if (fin == gridDim.x - 1u) {
-                p.rtail[0] = 0u;
-                p.rtail[kRenderTailDone] = 0u;
         }
 }
 
@@ -2296,7 +2225,7 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // with compaction: the rays still walking when fewer than t_first
         // lanes are go to queue 0 (SpillQueues)
-        const uint32_t t = kAny ? spill_reserve(p.sq, p.sq.ctr, p.sq.fill[0], cur, p.sq.t_first) : 0u;
+        const uint32_t t = kAny ? spill_threshold(p.sq, cur, p.sq.t_first) : 0u;
         bool hit = false, spilled = false;
         OcclState w;
         f3 dn;
@@ -2319,8 +2248,24 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
                         if (p.s_vox) p.s_vox[si] = m.hit ? p.sc.node_vox[m.node] : 0xFFFFFFFFu;
                 }
         }
-        if (kAny && t)
-                spill_group<kS>(p.sq.rec[0], cur, spilled, (uint32_t)pix, (uint32_t)vi, (uint32_t)lane, dn, w, stk);
+        if (kAny && t) {
+                const uint64_t sm0 = __ballot(spilled);
+                if (sm0 != 0ull) {
+                        if (spill_room(p.sq, p.sq.ctr, p.sq.fill[0], cur, (uint32_t)__popcll(sm0))) {
+                                spill_group<kS>(p.sq.rec[0], cur, spilled, (uint32_t)pix, (uint32_t)vi,
+                                                (uint32_t)lane, dn, w, stk);
+                        } else if (spilled) {
+                                // the queue is full: the ray walks on in place from where
+                                // it stopped (its state and LDS stack are intact), to its end
+                                const RayK r = make_rayk(mk3(pr[1], pr[2], pr[3]), dn, p.res, kFltMax);
+                                const int res = occl_dispatch_spill<kS, kR64>(p.sc, r, stk, w, true, 0u);
+                                hit = res == kOcclHit;
+                                spilled = false;
+                                if (p.s_hit)
+                                        p.s_hit[vi * (size_t)p.spp + lane] = hit ? 1 : 0;
+                        }
+                }
+        }
         const uint64_t hm = __ballot(hit);
         const uint64_t sm = kAny ? __ballot(spilled) : 0ull;
         if (lane == 0) {
@@ -3021,28 +2966,6 @@ hipError_t launch_selftest_order(const float *dist, const uint32_t *hm, int64_t 
         return hipGetLastError();
 }
 
-// Budgeted primary walks (k_render_p<true, kBudget> + k_render_tail): a
-// walk that would pass VRT_RENDER_BUDGET triangle tests stops and its pixel
-// is re-rendered by k_render_tail with 8 lanes per ray, so a unit of long
-// rays no longer holds one wave for its whole walk.  0 = off; by default only
-// for the shares of a multi-rank frame (VRT_RENDER_BUDGET_MULTI_ONLY), whose
-// frames are short enough that one such unit sets the frame's end.
-#ifndef VRT_RENDER_BUDGET
-#define VRT_RENDER_BUDGET 0
-#endif
-#ifndef VRT_RENDER_BUDGET_MULTI_ONLY
-#define VRT_RENDER_BUDGET_MULTI_ONLY 1
-#endif
-#ifndef VRT_RENDER_TAIL_GRID
-#define VRT_RENDER_TAIL_GRID 1024
-#endif
-bool render_uses_tail(const RenderParams &p)
-{
-        return VRT_RENDER_BUDGET > 0 && p.rtail && (!VRT_RENDER_BUDGET_MULTI_ONLY || p.nranks > 1) &&
-               render_kind(p, false) == kRenderPersistFast;
-}
-bool render_budget_built() { return VRT_RENDER_BUDGET > 0; }
-
 // persistent waves for RefRec48 scenes without per-sample outputs;
 // large-leaf (RefRec64) scenes keep one-wave workgroups (-11 % persistent at
 // depth 6).  The fast-only kernel when the camera makes standard-range
@@ -3202,15 +3125,6 @@ hipError_t persistent_blocks(int *render_blocks, int *sec_blocks)
         if (e != hipSuccess)
                 return e;
         *render_blocks = std::min(a, b);
-#if VRT_RENDER_BUDGET > 0
-        {
-                const int c = resident_blocks(reinterpret_cast<const void *>(k_render_p<true, VRT_RENDER_BUDGET>),
-                                              kPersistBlock, prop, &e);
-                if (e != hipSuccess)
-                        return e;
-                *render_blocks = std::min(*render_blocks, c);
-        }
-#endif
         int sb = 1 << 30;
         const void *sk[4] = { reinterpret_cast<const void *>(k_secondary_p<false, false>),
                               reinterpret_cast<const void *>(k_secondary_p<false, true>),
@@ -3243,20 +3157,9 @@ hipError_t launch_render(const RenderParams &p, bool instrumented,
                 const int cap = std::max(8, p.nranks > 1 ? full - kCollectiveReserve : full);
                 const int g = std::min(cap, need);
                 if (kind == kRenderPersistFast) {
-                        const bool tail = render_uses_tail(p);
-                        (void)tail;  // no budget built: never true
-                        void (*kern)(RenderParams) = k_render_p<true>;
-#if VRT_RENDER_BUDGET > 0
-                        if (tail)
-                                kern = k_render_p<true, VRT_RENDER_BUDGET>;
-#endif
-                        hipLaunchKernelGGL(kern, dim3(g), dim3(kPersistBlock), 0, st, p);
+                        hipLaunchKernelGGL(k_render_p<true>, dim3(g), dim3(kPersistBlock), 0, st, p);
                         if (hipError_t e = hipGetLastError())
                                 return e;
-#if VRT_RENDER_BUDGET > 0
-                        if (tail)
-                                hipLaunchKernelGGL(k_render_tail<false>, dim3(VRT_RENDER_TAIL_GRID), dim3(64), 0, st, p);
-#endif
 #if VRT_UNIT_DIAG
                         {
                                 static int ndump = 0;
@@ -4368,7 +4271,6 @@ bool build_flag(const char *name, int64_t *value)
                 { "VRT_DEAL_WEIGHT", VRT_DEAL_WEIGHT },
                 { "VRT_LIGHT_BUDGET", VRT_LIGHT_BUDGET },
                 { "VRT_PRIM_BUDGET", VRT_PRIM_BUDGET },
-                { "VRT_RENDER_BUDGET", VRT_RENDER_BUDGET },
         };
         for (const auto &f : kFlags)
                 if (std::strcmp(f.name, name) == 0) {
