@@ -667,12 +667,6 @@ def main():
         # in-place views (a rehearsal's 1-rank group gathers into row 0 only)
         gl = [list(g[:world].unbind(0)) for g in gathered] if rank == 0 else [None] * nbuf
     works = [None] * nbuf
-    # a frame's collective completion (and on rank 0 its re-assembly) is
-    # tracked on a side stream, never on the render streams: a render waits
-    # only for the collective that last read the buffer it reuses (buf_free)
-    post = torch.cuda.Stream(dev)
-    buf_free = [torch.cuda.Event() for _ in range(nbuf)]
-    buf_used = [False] * nbuf
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(a.steps)]
     # N-rank diagnostics on every DIAG_EVERY-th timed frame (each event record
@@ -690,14 +684,18 @@ def main():
         """frame k's stream slot and buffer slot"""
         return k % nfl, k % nbuf
 
-    def finish(b):
-        """Buffer b's collective complete on the side stream; rank 0 then
-        re-assembles the frame there; buf_free[b] marks the buffer free."""
+    def finish(b, s):
+        """Frame in buffer b: its collective complete on stream s (a stream
+        wait, no host block); rank 0 then re-assembles the frame there.  Called
+        on the stream of frame k with the buffer of frame k - nfl (the same
+        stream's previous frame), right after frame k's render is queued, so
+        no render waits for a collective -- only for the re-assembly queued
+        behind the previous render on its own stream (rank 0), and the buffer
+        is reused (frame k - nfl + nbuf, same stream) after it."""
         if works[b] is None:
             return
-        s = post
         with torch.cuda.stream(s):
-            works[b].wait()  # stream-wait on the collective, no host block
+            works[b].wait()
         works[b] = None
         k = frame_of[b]
         frame_of[b] = None
@@ -718,15 +716,6 @@ def main():
             if k is not None:
                 ev_unp[k][1].record(s)
                 unp_done.append(k)
-        buf_free[b].record(s)
-        buf_used[b] = True
-
-    def reuse(b, s):
-        """Before a frame renders into buffer b on stream s: the collective
-        (and unpack) of the frame that used b last have finished."""
-        finish(b)  # normally done already
-        if buf_used[b]:
-            s.wait_event(buf_free[b])
 
     def step_secondary(k, timed):
         cam = cams[k % a.poses]
@@ -740,7 +729,7 @@ def main():
             if timed:
                 ev[k][1].record(s)
             return
-        reuse(b, s)  # frame k - nbuf used these buffers
+        finish(b, s)  # frame k - nbuf used these buffers (finished already, same stream)
         if rank == 0:
             with torch.cuda.stream(s):
                 visb[b].zero_()  # the previous reduce summed into rank 0's buffer
@@ -754,7 +743,7 @@ def main():
             with torch.cuda.stream(s):
                 works[b] = dist.reduce(visb[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
             frame_of[b] = k if (timed and k % DIAG_EVERY == 0) else None
-            finish(sl(k - 1)[1])  # frame k-1: its reduce overlapped this render
+            finish(sl(k - nfl)[1], s)  # this stream's previous frame: its reduce overlapped this render
         else:
             host = visb[b].cpu()
             dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
@@ -782,7 +771,7 @@ def main():
             if timed:
                 ev[k][1].record(s)
             return
-        reuse(b, s)  # frame k - nbuf used this buffer pair
+        finish(b, s)  # frame k - nbuf used this buffer pair (finished already, same stream)
         render(cam, cur["share"], nshare, 0, tiles[b].data_ptr(), s)
         if timed:
             ev[k][1].record(s)
@@ -795,7 +784,7 @@ def main():
             with torch.cuda.stream(s):
                 works[b] = dist.gather(tiles[b], gl[b], dst=0, async_op=True)
             frame_of[b] = k if (timed and k % DIAG_EVERY == 0) else None
-            finish(sl(k - 1)[1])  # frame k-1: its gather overlapped this render
+            finish(sl(k - nfl)[1], s)  # this stream's previous frame: its gather overlapped this render
         else:  # gloo rehearsal (several ranks on one GPU): host-staged gather
             host = tiles[b].cpu()
             hl = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
@@ -806,7 +795,7 @@ def main():
 
     def drain():
         for b in range(nbuf):
-            finish(b)
+            finish(b, stream)
 
     def timed_run():
         """W warm-up steps, then K timed steps between barrier + synchronize

@@ -173,7 +173,7 @@ int vrt_render(vrt_scene *s, const vrt_camera *cam, const vrt_film *film,
  * G = vrt_tile_deal_block() (G = 1 when nranks == 1), the whole G x G blocks
  * of tiles are dealt round-robin in block raster order (block j -> rank
  * j % nranks; from 4 ranks on rank 0, which also gathers and re-assembles,
- * is dealt (m-1)/m of a share, m = max(2, 64/nranks): block j -> rank
+ * is dealt (m-1)/m of a share, m = max(2, 48/nranks): block j -> rank
  * nranks-1 - (j % V) % nranks with V = m*nranks - 1, a rank's blocks in
  * raster order); the tiles outside the whole-block region -- the right strip
  * (rows ty < G*(nty/G), columns tx >= G*(ntx/G)), then the bottom strip, each

@@ -103,7 +103,7 @@ def test_c2_1080p_depth8_whole_frame(proxy, pose):
 
 def test_c3_c4_4k_depth9_whole_frame_and_8_ranks(proxy):
     """C3 whole frame, then C4: the same frame as 8 ranks' tiles (the tile
-    deal of include/vrt.h: 4x4-tile blocks, rank 0 dealt 7/8 of a share),
+    deal of include/vrt.h: 4x4-tile blocks, rank 0 dealt 5/6 of a share),
     gathered rank-major and unpacked, equals it bit for bit."""
     tree, cam, film, orgb = _whole_frame(proxy, 9, 7, 3840, 2160)
     assert np.array_equal(bits(_device_image(tree, cam, film, nranks=8)), bits(orgb))

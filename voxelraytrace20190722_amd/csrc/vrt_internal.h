@@ -253,7 +253,9 @@ struct SpillQueues {
 //
 // Rank 0 lighter (VRT_DEAL_WEIGHT, nranks >= 4): rank 0 also gathers and
 // re-assembles the frame, so it is dealt (m-1)/m of another rank's blocks,
-// m = max(2, 64 / nranks) (7/8 at 8 ranks, 15/16 at 4).  The whole blocks
+// m = max(2, VRT_DEAL_SPAN / nranks) (5/6 at 8 ranks, 11/12 at 4: round 5,
+// from every rank's rehearsed step; 7/8 and 15/16 with span 64 left rank 0
+// the slowest once the collective no longer delayed the other ranks).  The whole blocks
 // then run in periods of V = m*nranks - 1: position pos = j % V of block j
 // goes to rank nranks-1 - pos % nranks (ranks in descending order, rank 0's
 // last turn of the period left out); a rank's blocks keep raster order.
@@ -262,6 +264,9 @@ struct SpillQueues {
 #endif
 #ifndef VRT_DEAL_WEIGHT
 #define VRT_DEAL_WEIGHT 1
+#endif
+#ifndef VRT_DEAL_SPAN
+#define VRT_DEAL_SPAN 48
 #endif
 struct TileDeal {
         int ntx, nty, nranks, G;
@@ -285,7 +290,7 @@ __host__ __device__ inline TileDeal tile_deal(int ntx, int nty, int nranks)
         d.rw = ntx - d.bx * d.G;
         d.nA = d.by * d.G * d.rw;
         d.L = ntx * nty - d.F * d.G * d.G;
-        d.m = VRT_DEAL_WEIGHT && nranks >= 4 ? (64 / nranks > 2 ? 64 / nranks : 2) : 0;
+        d.m = VRT_DEAL_WEIGHT && nranks >= 4 ? (VRT_DEAL_SPAN / nranks > 2 ? VRT_DEAL_SPAN / nranks : 2) : 0;
         d.V = d.m ? d.m * nranks - 1 : 0;
         return d;
 }

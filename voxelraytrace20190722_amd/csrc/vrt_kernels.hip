@@ -4269,6 +4269,7 @@ bool build_flag(const char *name, int64_t *value)
                 { "VRT_SLICE_CHUNK", VRT_SLICE_CHUNK },
                 { "VRT_DEAL_BLOCK", VRT_DEAL_BLOCK },
                 { "VRT_DEAL_WEIGHT", VRT_DEAL_WEIGHT },
+                { "VRT_DEAL_SPAN", VRT_DEAL_SPAN },
                 { "VRT_LIGHT_BUDGET", VRT_LIGHT_BUDGET },
                 { "VRT_PRIM_BUDGET", VRT_PRIM_BUDGET },
         };

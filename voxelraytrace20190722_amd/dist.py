@@ -38,12 +38,12 @@ def deal_block():
 def deal_weight(nranks):
     """(m, V) of the weighted deal (vrt_internal.h VRT_DEAL_WEIGHT): from 4
     ranks on, rank 0 -- which also gathers and re-assembles the frame -- gets
-    (m-1)/m of another rank's blocks, m = max(2, 64 // nranks); the whole
+    (m-1)/m of another rank's blocks, m = max(2, 48 // nranks); the whole
     blocks run in periods of V = m*nranks - 1 turns, position p of a period
     going to rank nranks-1 - p % nranks.  (0, 0): plain round robin."""
     if nranks < 4:
         return 0, 0
-    m = max(2, 64 // nranks)
+    m = max(2, 48 // nranks)
     return m, m * nranks - 1
 
 
