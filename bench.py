@@ -348,8 +348,9 @@ def per_rank_report(world, backend, dev, rank, vals):
     (all_gather: each rank calls) -> the per-rank list rank 0 prints.  share:
     the mean render span of this rank's share (HIP events on its stream);
     collective: from the end of the render to the frame's gather / reduce
-    being complete on the stream that waits for it; unpack: rank 0's
-    re-assembly kernel (0 elsewhere)."""
+    being waited for on its stream (queued behind that stream's next render,
+    so it includes that render); unpack: rank 0's re-assembly kernel (0
+    elsewhere)."""
     t = torch.tensor([float(rank)] + [float(v) for v in vals], dtype=torch.float64,
                      device=dev if backend == "nccl" else "cpu")
     out = [torch.zeros_like(t) for _ in range(world)]
