@@ -172,7 +172,7 @@ int vrt_render(vrt_scene *s, const vrt_camera *cam, const vrt_film *film,
  * The tile deal (one rule for every multi-rank entry point): with
  * G = vrt_tile_deal_block() (G = 1 when nranks == 1), the whole G x G blocks
  * of tiles are dealt round-robin in block raster order (block j -> rank
- * j % nranks; from 4 ranks on rank 0, which also gathers and re-assembles,
+ * j % nranks; from 2 ranks on rank 0, which also gathers and re-assembles,
  * is dealt (m-1)/m of a share, m = max(2, 48/nranks): block j -> rank
  * nranks-1 - (j % V) % nranks with V = m*nranks - 1, a rank's blocks in
  * raster order); the tiles outside the whole-block region -- the right strip
@@ -281,10 +281,6 @@ int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
 /* VRT_TEST_PRIM_TAIL does the same for the primary pass of the cone-traced
  * render (vrt_render_trace*, vrt_trace_frame_device). */
 #define VRT_TEST_PRIM_TAIL 64
-/* VRT_TEST_NO_STREAM makes config 5's resume round walk queue 0 chunk by
- * chunk (k_sec_resume) instead of streaming it -- the path of films of 2^26
- * pixels or more. */
-#define VRT_TEST_NO_STREAM 128
 #define VRT_TEST_VIRTUAL_RANKS_N(n) (VRT_TEST_VIRTUAL_RANKS | ((n) << 8))
 int vrt_set_test_flags(int flags);
 /* The current vrt_set_test_flags value (so a caller can restore it). */

@@ -366,8 +366,7 @@ def test_secondary_occlusion_walk_matches_ordered_walk(proxy_small, depth):
 
 @pytest.mark.parametrize("depth", [6, 8])
 @pytest.mark.parametrize("flags,spp", [(0, 64), (vrt.TEST_SPILL_ALL, 64), (0, 17), (0, 1),
-                                       (vrt.TEST_SPILL_ALL | vrt.TEST_STREAM_LEFTOVER, 64),
-                                       (vrt.TEST_SPILL_ALL | vrt.TEST_NO_STREAM, 64), (vrt.TEST_NO_STREAM, 17)])
+                                       (vrt.TEST_SPILL_ALL | vrt.TEST_STREAM_LEFTOVER, 64)])
 def test_secondary_compaction_matches_oracle(proxy_small, depth, flags, spp):
     """Config-5 ray compaction: rays still walking when few
     lanes of their wave are go to a queue with their walk state and are
@@ -377,10 +376,9 @@ def test_secondary_compaction_matches_oracle(proxy_small, depth, flags, spp):
     saved and resumed mid-walk at least once: the resume round walks them 64 to
     a wave as one stream: a pool of subtree pieces handed to idle lanes, a
     slot refilled with the next saved ray as soon as its ray ends
-    (resume_stream, VRT_SEC_STREAM); TEST_STREAM_LEFTOVER sends every odd
-    chunk to the batch pool (occl_pool) launched after it; TEST_NO_STREAM
-    walks queue 0 chunk by chunk (k_sec_resume: films of 2^26 pixels or
-    more); spp < 64 starts with idle lanes."""
+    (resume_stream); TEST_STREAM_LEFTOVER sends every odd
+    chunk to the batch pool (occl_pool) launched after it; spp < 64 starts
+    with idle lanes."""
     tree = vrt.VoxelOctree(proxy_small, depth)
     osc = po.Scene(proxy_small, depth)
     mn, mx = tree.root_box

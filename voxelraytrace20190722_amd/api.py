@@ -730,7 +730,6 @@ TEST_VIRTUAL_RANKS = 8  # include/vrt.h VRT_TEST_VIRTUAL_RANKS (count << 8)
 TEST_STREAM_LEFTOVER = 16  # include/vrt.h VRT_TEST_STREAM_LEFTOVER
 TEST_LIGHT_TAIL = 32  # include/vrt.h VRT_TEST_LIGHT_TAIL
 TEST_PRIM_TAIL = 64  # include/vrt.h VRT_TEST_PRIM_TAIL
-TEST_NO_STREAM = 128  # include/vrt.h VRT_TEST_NO_STREAM
 
 
 def set_test_flags(flags):

@@ -1316,23 +1316,26 @@ static int ts_release(vrt_scene *s, int i, hipStream_t st);
 // size is an estimate: when the queue is full, the rays that stop finish
 // their walks in place (spill_room), so any size gives the same images.  The
 // first launch sizes queue 0 for 1/32 of the rank's secondary rays (1080p:
-// 4.1 M records, 0.5 GiB) plus one partly filled chunk per resident wave;
-// after every launch its counters are copied to pinned memory, and a later
-// launch sizes for 1.25 x the records its phase A stopped (queued + finished
-// in place), growing, never shrinking.  Only
-// queue 0's records are allocated: the one pooled resume round walks every
-// saved ray to its end (queue 1's fill words list the streaming round's
+// 4.1 M 64-B records, 0.26 GB) plus one partly filled chunk per resident
+// wave; after every launch its counters are copied to pinned memory, and a
+// later launch sizes for 1.25 x the records its phase A stopped (queued +
+// finished in place), growing, never shrinking, and never past 1 GiB per set.
+// Only queue 0's records are allocated: the one pooled resume round walks
+// every saved ray to its end (queue 1's fill words list the streaming round's
 // leftover chunks).  The scene keeps two sets; a stream keeps using the set
-// it used last (stream order protects it), a new stream takes the other one
-// (frames in flight on two streams), waiting for its last user's event.
-// sq->nchunks stays 0 (no compaction) when the build disables it or the
-// allocation fails.
-constexpr uint32_t kSpillCapMax = (1u << 24) / kSpillChunk;  // chunks: 2 GiB of records at most
-static int spill_setup(vrt_scene *s, int64_t rays, hipStream_t st, SpillQueues *sq, int *set)
+// it used last (stream order protects it), an idle set is shared, and a
+// second set is allocated only for frames in flight on two streams (the new
+// stream waits for the set's last user's event).  sq->nchunks stays 0 (no
+// compaction) when the build disables it, the film has 2^26 pixels or more,
+// the octree 2^24 nodes or more (SpillRec's packed words), or the allocation
+// fails.
+constexpr uint32_t kSpillCapMax = (uint32_t)((size_t)1 << 30) / (kSpillChunk * (uint32_t)sizeof(SpillRec));  // chunks
+static int spill_setup(vrt_scene *s, int64_t rays, int64_t pixels, hipStream_t st, SpillQueues *sq, int *set)
 {
         *sq = spill_defaults();
         *set = -1;
-        if (sq->t_first == 0 || rays <= 0)
+        // SpillRec packs the pixel in 26 bits and a stack entry's block in 24
+        if (sq->t_first == 0 || rays <= 0 || pixels >= (int64_t)1 << 26 || s->nodes.size() >= ((size_t)1 << 24))
                 return VRT_OK;
         // this stream's own set; else an allocated set whose last launch has
         // finished (a second set is allocated only for frames in flight on
@@ -1429,7 +1432,7 @@ static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int ra
                         return rc;
                 if (!s_tri && !s_vox) {  // the occlusion walk: compaction
                         const int64_t rays = deal_count(tile_deal(p.ntx, p.nty, nranks), rank) * 64 * (int64_t)spp;
-                        if (int rc = spill_setup(s, rays, st, &sq, &set))
+                        if (int rc = spill_setup(s, rays, (int64_t)p.ntx * 8 * p.nty * 8, st, &sq, &set))
                                 return rc;
                 }
         }

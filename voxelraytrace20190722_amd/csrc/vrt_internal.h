@@ -215,28 +215,30 @@ __host__ __device__ inline int slice_unit(int units, int x, int u, int ch)
 // when it moves on; a resume wave takes one chunk at a time.
 constexpr int kSpillStack = 10;  // >= the DFS stack (kStack, vrt_kernels.hip)
 constexpr uint32_t kSpillChunk = 256;
+// 64 B.  The compaction runs only for films under 2^26 pixels and octrees
+// under 2^24 nodes (spill_setup), so a pixel and a DFS stack entry each fit a
+// word.
 struct alignas(16) SpillRec {
-        uint32_t pix;    // y * W8 + x (primary record index)
-        uint32_t vi;     // y * nx + x (visibility image index)
-        uint32_t sample; // secondary ray index (s_hit)
-        uint32_t sp;     // stack entries
-        float d[3];      // normalised direction (the ray's origin is the pixel's hit point)
-        uint32_t pad;
-        uint32_t base, mask, pad2, pad3;
-        uint32_t stk[2 * kSpillStack];
+        uint32_t pix_smp;  // primary record index (y * W8 + x) | secondary ray index << 26
+        uint32_t base;     // the child block the walk was in
+        uint32_t mask_sp;  // its children left to visit (8 bits) | stack entries << 8
+        float d[3];        // normalised direction (the ray's origin is the pixel's hit point)
+        uint32_t stk[kSpillStack];  // DFS stack, bottom first: block << 8 | children left
 };
-static_assert(sizeof(SpillRec) == 128, "SpillRec layout");
+static_assert(sizeof(SpillRec) == 64, "SpillRec layout");
 constexpr int kSpillCtrStride = 32;  // one 128-B line per round's counters
 constexpr int kSpillMaxRounds = 4;
 struct SpillQueues {
-        uint32_t *ctr;       // round r: [r*stride + 0] chunks taken by its writers,
-                             // [r*stride + 1] chunks taken by round r+1, [r*stride + 2]
-                             // records written (zeroed per frame)
-        uint32_t *fill[2];   // records in each chunk of queue r (fill[r & 1]), written by the chunk's writer
-        SpillRec *rec[2];    // queue r's records: rec[r & 1] + chunk * kSpillChunk
-        uint32_t nchunks;    // chunks per queue; 0 = no compaction
+        uint32_t *ctr;       // zeroed per frame: [0] chunks taken by phase A, [1] chunks taken by the
+                             // stream, [2] records written, [3] chunks the stream left to k_sec_resume,
+                             // [4] their pieces taken, [5] stopped rays finished in place (queue full);
+                             // the words of rounds 1..3 ([r * kSpillCtrStride + 2]) stay 0
+        uint32_t *fill[2];   // [0] records in each chunk of queue 0, written by the chunk's writer;
+                             // [1] the chunks the stream left
+        SpillRec *rec[2];    // queue 0's records: rec[0] + chunk * kSpillChunk ([1] unused)
+        uint32_t nchunks;    // chunks in queue 0; 0 = no compaction
         uint32_t t_first;    // phase-A threshold (walking lanes)
-        int32_t stream;      // the resume round streams its rays (VRT_SEC_STREAM; films < 2^26 pixels)
+        int32_t stream;      // 1: the resume round streams queue 0 (the only mode)
 };
 
 // Tile deal of a multi-rank frame.  The ntx x nty grid of
@@ -251,11 +253,12 @@ struct SpillQueues {
 // (rays of one region walk the same part of the octree), and every rank gets
 // the same number of blocks +-1.  G = 1 is tile t -> rank t % nranks.
 //
-// Rank 0 lighter (VRT_DEAL_WEIGHT, nranks >= 4): rank 0 also gathers and
+// Rank 0 lighter (VRT_DEAL_WEIGHT, nranks >= 2): rank 0 also gathers and
 // re-assembles the frame, so it is dealt (m-1)/m of another rank's blocks,
-// m = max(2, VRT_DEAL_SPAN / nranks) (5/6 at 8 ranks, 11/12 at 4: round 5,
-// from every rank's rehearsed step; 7/8 and 15/16 with span 64 left rank 0
-// the slowest once the collective no longer delayed the other ranks).  The whole blocks
+// m = max(2, VRT_DEAL_SPAN / nranks) (5/6 at 8 ranks, 11/12 at 4, 23/24 at 2:
+// round 5, from every rank's rehearsed step; 7/8 and 15/16 with span 64, and
+// no weighting below 4 ranks, left rank 0 the slowest once the collective
+// no longer delayed the other ranks).  The whole blocks
 // then run in periods of V = m*nranks - 1: position pos = j % V of block j
 // goes to rank nranks-1 - pos % nranks (ranks in descending order, rank 0's
 // last turn of the period left out); a rank's blocks keep raster order.
@@ -290,7 +293,7 @@ __host__ __device__ inline TileDeal tile_deal(int ntx, int nty, int nranks)
         d.rw = ntx - d.bx * d.G;
         d.nA = d.by * d.G * d.rw;
         d.L = ntx * nty - d.F * d.G * d.G;
-        d.m = VRT_DEAL_WEIGHT && nranks >= 4 ? (VRT_DEAL_SPAN / nranks > 2 ? VRT_DEAL_SPAN / nranks : 2) : 0;
+        d.m = VRT_DEAL_WEIGHT && nranks >= 2 ? (VRT_DEAL_SPAN / nranks > 2 ? VRT_DEAL_SPAN / nranks : 2) : 0;
         d.V = d.m ? d.m * nranks - 1 : 0;
         return d;
 }

@@ -1537,19 +1537,36 @@ __device__ __forceinline__ uint64_t occl_pool(const DevScene &sc, f3 o, const fl
         return hitm;
 }
 
-// One stopped ray's record (SpillRec): its pixel, sample, direction and walk
-// state, the stack entries copied out of the lane's LDS column.
+// One stopped ray's record (SpillRec, 64 B): its pixel and sample, walk
+// state and direction, the stack entries copied out of the lane's LDS column
+// (block << 8 | children left: blocks < 2^24, spill_setup).
 template <int kS>
-__device__ __forceinline__ void spill_write(SpillRec *o, uint32_t pix, uint32_t vi, uint32_t sample, f3 d,
-                                            const OcclState &w, const uint2 *stk)
+__device__ __forceinline__ void spill_write(SpillRec *o, uint32_t pix, uint32_t sample, f3 d, const OcclState &w,
+                                            const uint2 *stk)
 {
         uint4 *q = reinterpret_cast<uint4 *>(o);
-        q[0] = make_uint4(pix, vi, sample, (uint32_t)w.sp);
-        q[1] = make_uint4(__float_as_uint(d.x), __float_as_uint(d.y), __float_as_uint(d.z), 0u);
-        q[2] = make_uint4(w.base, w.mask, 0u, 0u);
-        uint2 *e = reinterpret_cast<uint2 *>(o->stk);
-        for (int k = 0; k < w.sp; ++k)
-                e[k] = stk[k * kS];
+        q[0] = make_uint4(pix | sample << 26, w.base, w.mask | (uint32_t)w.sp << 8, __float_as_uint(d.x));
+        q[1].x = __float_as_uint(d.y);
+        q[1].y = __float_as_uint(d.z);
+        for (int k = 0; k < w.sp; ++k) {
+                const uint2 e = stk[k * kS];
+                o->stk[k] = e.x << 8 | e.y;
+        }
+}
+
+// A record's walk state back: (pix | sample << 26, base, mask | sp << 8, d)
+// into h / d, its stack entries into the lane's LDS column (stride kS).
+template <int kS>
+__device__ __forceinline__ void spill_read(const SpillRec *q, uint4 &h, f3 &d, uint2 *stk)
+{
+        h = reinterpret_cast<const uint4 *>(q)[0];
+        const uint2 t = reinterpret_cast<const uint2 *>(q)[2];
+        d = mk3(__uint_as_float(h.w), __uint_as_float(t.x), __uint_as_float(t.y));
+        const int sp = (int)(h.z >> 8);
+        for (int k = 0; k < sp; ++k) {
+                const uint32_t e = q->stk[k];
+                stk[k * kS] = make_uint2(e >> 8, e & 0xFFu);
+        }
 }
 
 // lane 0 adds n to *ctr, the wave reads lane 0's result (as take_unit)
@@ -1616,7 +1633,7 @@ __device__ __forceinline__ bool spill_room(const SpillQueues &q, uint32_t *ctr, 
 // The stopped rays of a group (`spilled`, after the walks): each writes its
 // record at the cursor's next free slots in lane order.
 template <int kS>
-__device__ __forceinline__ void spill_group(SpillRec *rec, SpillCursor &c, bool spilled, uint32_t pix, uint32_t vi,
+__device__ __forceinline__ void spill_group(SpillRec *rec, SpillCursor &c, bool spilled, uint32_t pix,
                                             uint32_t sample, f3 d, const OcclState &w, const uint2 *stk)
 {
         const uint64_t sm = __ballot(spilled);
@@ -1625,7 +1642,7 @@ __device__ __forceinline__ void spill_group(SpillRec *rec, SpillCursor &c, bool 
         if (spilled) {
                 const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-                spill_write<kS>(rec + (size_t)c.chunk * kSpillChunk + c.fill + below, pix, vi, sample, d, w, stk);
+                spill_write<kS>(rec + (size_t)c.chunk * kSpillChunk + c.fill + below, pix, sample, d, w, stk);
         }
         c.fill += (uint32_t)__popcll(sm);
 }
@@ -2252,8 +2269,8 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
                 const uint64_t sm0 = __ballot(spilled);
                 if (sm0 != 0ull) {
                         if (spill_room(p.sq, p.sq.ctr, p.sq.fill[0], cur, (uint32_t)__popcll(sm0))) {
-                                spill_group<kS>(p.sq.rec[0], cur, spilled, (uint32_t)pix, (uint32_t)vi,
-                                                (uint32_t)lane, dn, w, stk);
+                                spill_group<kS>(p.sq.rec[0], cur, spilled, (uint32_t)pix, (uint32_t)lane, dn, w,
+                                                stk);
                         } else if (spilled) {
                                 // the queue is full: the ray walks on in place from where
                                 // it stopped (its state and LDS stack are intact), to its end
@@ -2288,7 +2305,7 @@ struct ResumeParams {
         int32_t *s_hit;
         int32_t spp;
         float res;
-        int32_t nx, W8;  // pixel index <-> primary record index (VRT_SEC_STREAM)
+        int32_t nx, W8;  // pixel index <-> primary record index
         int32_t test_flags;
         SpillQueues sq;
 };
@@ -2310,18 +2327,11 @@ __device__ __forceinline__ void resume_pool_chunk(const ResumeParams &p, const S
                 uint4 h0 = reinterpret_cast<const uint4 *>(rec + g)[0];  // lanes past the fill: a valid pixel
                 f3 dn = mk3(0.f, 0.f, 1.f);
                 if (i < fill) {
-                        const SpillRec *q = rec + i;
-                        h0 = reinterpret_cast<const uint4 *>(q)[0];
-                        const uint4 h1 = reinterpret_cast<const uint4 *>(q)[1];
-                        const uint4 h2 = reinterpret_cast<const uint4 *>(q)[2];
-                        sp = (int)h0.w;
-                        base = h2.x;
-                        mask = h2.y;
-                        const uint2 *e = reinterpret_cast<const uint2 *>(q->stk);
-                        for (int k = 0; k < sp; ++k)
-                                stk[k * kSecPBlock] = e[k];
-                        dn = mk3(__uint_as_float(h1.x), __uint_as_float(h1.y), __uint_as_float(h1.z));
-                        const float *pr = p.prim + 8 * (size_t)h0.x;
+                        spill_read<kSecPBlock>(rec + i, h0, dn, stk);
+                        sp = (int)(h0.z >> 8);
+                        base = h0.y;
+                        mask = h0.z & 0xFFu;
+                        const float *pr = p.prim + 8 * (size_t)(h0.x & 0x3FFFFFFu);
                         const RayK r = make_rayk(mk3(pr[1], pr[2], pr[3]), dn, p.res, kFltMax);
                         ok = p.sc.fast_ok && fast_ok(r) && fin_ok(r);
                         busy = true;
@@ -2329,7 +2339,8 @@ __device__ __forceinline__ void resume_pool_chunk(const ResumeParams &p, const S
                 dirs[lane][0] = dn.x;
                 dirs[lane][1] = dn.y;
                 dirs[lane][2] = dn.z;
-                opix[lane] = h0.x;
+                const uint32_t pix = h0.x & 0x3FFFFFFu, smp = h0.x >> 26;
+                opix[lane] = pix;
                 wave_lds_sync();
                 const uint64_t hm =
                         __all(ok) ? occl_pool<true, kSecPBlock, kR64, true, true>(
@@ -2340,12 +2351,13 @@ __device__ __forceinline__ void resume_pool_chunk(const ResumeParams &p, const S
                                             busy, base, mask, sp, 0ull);
                 if (i < fill) {
                         const uint32_t hit = (uint32_t)((hm >> lane) & 1ull);
+                        const uint32_t vi = (pix / (uint32_t)p.W8) * (uint32_t)p.nx + pix % (uint32_t)p.W8;
                         if (p.s_hit)
-                                p.s_hit[(size_t)h0.y * (size_t)p.spp + h0.z] = (int32_t)hit;
-                        float *pr = p.prim + 8 * (size_t)h0.x;
+                                p.s_hit[(size_t)vi * (size_t)p.spp + smp] = (int32_t)hit;
+                        float *pr = p.prim + 8 * (size_t)pix;
                         const uint32_t old = atomicAdd(reinterpret_cast<uint32_t *>(pr) + 7, hit ? 255u : 0xFFFFFFFFu);
                         if ((old & 0xFFu) == 1u)  // the pixel's last ray
-                                p.vis[h0.y] = (float)(p.spp - (int)((old >> 8) + hit)) / (float)p.spp;
+                                p.vis[vi] = (float)(p.spp - (int)((old >> 8) + hit)) / (float)p.spp;
                 }
                 wave_lds_sync();  // dirs / opix / mbox / hword are rewritten by the next batch
         }
@@ -2353,7 +2365,7 @@ __device__ __forceinline__ void resume_pool_chunk(const ResumeParams &p, const S
 
 
 // ---------------------------------------------------------------------------
-// VRT_SEC_STREAM: the resume round as one stream per wave.  The wave's lanes
+// The resume round as one stream per wave.  The wave's lanes
 // are a pool over 64 slots (as occl_pool), but a slot whose ray has ended is
 // refilled at once with the next saved ray of the queue (chunks taken with
 // take_n), so lanes idle only when no piece can be handed over AND the
@@ -2389,10 +2401,10 @@ __device__ __forceinline__ bool stream_chunk_fast(const ResumeParams &p, const S
         bool ok = !((p.test_flags & VRT_TEST_STREAM_LEFTOVER) && (c & 1u));  // test hook: odd chunks left over
         for (uint32_t i = lane; i < fill; i += 64) {
                 const uint4 h0 = reinterpret_cast<const uint4 *>(rec + i)[0];
-                const uint4 h1 = reinterpret_cast<const uint4 *>(rec + i)[1];
-                const float *pr = p.prim + 8 * (size_t)h0.x;
+                const uint2 t = reinterpret_cast<const uint2 *>(rec + i)[2];
+                const float *pr = p.prim + 8 * (size_t)(h0.x & 0x3FFFFFFu);
                 const RayK r = make_rayk(mk3(pr[1], pr[2], pr[3]),
-                                         mk3(__uint_as_float(h1.x), __uint_as_float(h1.y), __uint_as_float(h1.z)),
+                                         mk3(__uint_as_float(h0.w), __uint_as_float(t.x), __uint_as_float(t.y)),
                                          p.res, kFltMax);
                 ok = ok && p.sc.fast_ok && fast_ok(r) && fin_ok(r) && leaf_box_ok(p.sc, r);
         }
@@ -2504,24 +2516,19 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
                                         const uint32_t k = (uint32_t)__popcll(still & lt);
                                         if (k < ntake) {
                                                 slot = map[k];
-                                                const SpillRec *q = in + (size_t)chunk * kSpillChunk + cur + k;
-                                                const uint4 h0 = reinterpret_cast<const uint4 *>(q)[0];
-                                                const uint4 h1 = reinterpret_cast<const uint4 *>(q)[1];
-                                                const uint4 h2 = reinterpret_cast<const uint4 *>(q)[2];
-                                                sp = (int)h0.w;
+                                                uint4 h0;
+                                                f3 d;
+                                                spill_read<kSecPBlock>(in + (size_t)chunk * kSpillChunk + cur + k, h0,
+                                                                       d, stk);
+                                                sp = (int)(h0.z >> 8);
                                                 bot = 0;
-                                                base = h2.x;
-                                                mask = h2.y;
-                                                const uint2 *e = reinterpret_cast<const uint2 *>(q->stk);
-                                                for (int j = 0; j < sp; ++j)
-                                                        stk[j * kSecPBlock] = e[j];
-                                                const f3 d = mk3(__uint_as_float(h1.x), __uint_as_float(h1.y),
-                                                                 __uint_as_float(h1.z));
+                                                base = h0.y;
+                                                mask = h0.z & 0xFFu;
                                                 dirs[slot][0] = d.x;
                                                 dirs[slot][1] = d.y;
                                                 dirs[slot][2] = d.z;
-                                                sinfo[slot] = h0.x | (h0.z << 26);
-                                                const float *pr = p.prim + 8 * (size_t)h0.x;
+                                                sinfo[slot] = h0.x;  // pix | sample << 26
+                                                const float *pr = p.prim + 8 * (size_t)(h0.x & 0x3FFFFFFu);
                                                 r = make_rayk(mk3(pr[1], pr[2], pr[3]), d, p.res, kFltMax);
                                                 s = dir_signs(r);
                                                 busy = true;
@@ -2630,7 +2637,7 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
         }
 }
 
-// The streaming resume round (VRT_SEC_STREAM, films under 2^26 pixels): one
+// The streaming resume round (films under 2^26 pixels): one
 // resident generation, each wave one stream (resume_stream) over queue 0.
 #ifndef VRT_STREAM_WAVES_PER_EU
 #define VRT_STREAM_WAVES_PER_EU VRT_SECP_WAVES_PER_EU
@@ -2658,37 +2665,24 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_resum
         __shared__ uint2 mbox[kSecPBlock / 64][64];
         __shared__ unsigned long long hword[kSecPBlock / 64];
         const int tid = threadIdx.x;
-        uint32_t *cin = p.sq.ctr;
-        const uint32_t n = min(cin[0], p.sq.nchunks);  // queue 0's chunks (the walk launch's)
         const uint32_t *fin = p.sq.fill[0];
         const SpillRec *in = p.sq.rec[0];
-        // leftover mode (after k_sec_stream): the chunks it listed, from ctr[4],
-        // each as kSpillChunk / 64 pieces of 64 rays on different waves (the
-        // few leftover chunks of a frame would otherwise leave one wave
-        // walking a whole chunk's batches one after the other); otherwise
-        // (films of 2^26 pixels or more, whose pixel index does not fit
-        // resume_stream's slot word) every chunk of queue 0 whole
-        const bool left = p.sq.stream;
+        // the chunks k_sec_stream listed (normally none), from ctr[4], each as
+        // kSpillChunk / 64 pieces of 64 rays on different waves (the few
+        // leftover chunks of a frame would otherwise leave one wave walking a
+        // whole chunk's batches one after the other)
         constexpr uint32_t kParts = kSpillChunk / 64;
-        const uint32_t nl = left ? p.sq.ctr[3] * kParts : 0u;
+        const uint32_t nl = p.sq.ctr[3] * kParts;
         for (;;) {
-                uint32_t c, part = 0;
-                if (left) {
-                        const uint32_t j = take_n(p.sq.ctr + 4, 1u);
-                        if (j >= nl)
-                                break;
-                        c = __builtin_amdgcn_readfirstlane(p.sq.fill[1][j / kParts]);
-                        part = j % kParts;
-                } else {
-                        c = take_n(cin + 1, 1u);
-                        if (c >= n)
-                                break;
-                }
+                const uint32_t j = take_n(p.sq.ctr + 4, 1u);
+                if (j >= nl)
+                        break;
+                const uint32_t c = __builtin_amdgcn_readfirstlane(p.sq.fill[1][j / kParts]), part = j % kParts;
                 const int w = tid >> 6;
                 const uint32_t f = fin[c], lo = part * 64u;
                 if (lo >= f)
                         continue;
-                const uint32_t cnt = left ? min(64u, f - lo) : f;
+                const uint32_t cnt = min(64u, f - lo);
                 resume_pool_chunk<kR64>(p, in + (size_t)c * kSpillChunk + lo, cnt, stk + tid, dirs[w], opix[w],
                                         mbox[w], hword + w);
         }
@@ -2816,23 +2810,14 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                         rp2.test_flags = rp.test_flags;
                         rp2.W8 = rp.ntx * 8;
                         rp2.sq = sp.sq;
-                        // the streaming round (films under 2^26 pixels: resume_stream packs the
-                        // pixel index in 26 bits; VRT_TEST_NO_STREAM takes the other path)
-#ifndef VRT_SEC_STREAM
-#define VRT_SEC_STREAM 1
-#endif
-                        rp2.sq.stream = VRT_SEC_STREAM && (int64_t)rp.ntx * 8 * rp.nty * 8 < (1 << 26) &&
-                                        !(rp.test_flags & VRT_TEST_NO_STREAM);
-                        if (rp2.sq.stream) {
-                                hipLaunchKernelGGL(w ? k_sec_stream<true> : k_sec_stream<false>, dim3(g),
-                                                   dim3(kSecPBlock), 0, st, rp2);
-                                // the chunks the stream left (normally none): a small batch-pool launch
-                                hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(8),
-                                                   dim3(kSecPBlock), 0, st, rp2);
-                        } else {
-                                hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(g),
-                                                   dim3(kSecPBlock), 0, st, rp2);
-                        }
+                        // the streaming round (the host compacts only films under 2^26
+                        // pixels: resume_stream packs the pixel index in 26 bits)
+                        rp2.sq.stream = 1;
+                        hipLaunchKernelGGL(w ? k_sec_stream<true> : k_sec_stream<false>, dim3(g), dim3(kSecPBlock),
+                                           0, st, rp2);
+                        // the chunks the stream left (normally none): a small batch-pool launch
+                        hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(8), dim3(kSecPBlock), 0,
+                                           st, rp2);
                 }
                 return hipGetLastError();
         }
@@ -4262,7 +4247,6 @@ bool build_flag(const char *name, int64_t *value)
                 int64_t value;
         } kFlags[] = {
                 { "VRT_SEC_SPILL_T", VRT_SEC_SPILL_T },
-                { "VRT_SEC_STREAM", VRT_SEC_STREAM },
 
                 { "VRT_SEC_SLICE_CHUNK", VRT_SEC_SLICE_CHUNK },
 

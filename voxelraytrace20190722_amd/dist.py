@@ -11,7 +11,7 @@ The tile deal (include/vrt.h, vrt_internal.h `tile_deal`): the render area
 is the ntx x nty grid of 8x8-pixel tiles (ntx = nx//8, nty = ny//8).  With
 G = the library's deal block (G = 1 for one rank), the whole G x G blocks of
 tiles are dealt round-robin in block raster order (block j -> rank
-j % nranks; from 4 ranks on rank 0 gets fewer, see deal_weight); the tiles outside the whole-block region -- the right strip
+j % nranks; from 2 ranks on rank 0 gets fewer, see deal_weight); the tiles outside the whole-block region -- the right strip
 (rows above the bottom strip), then the bottom strip, each in raster order
 -- continue the deal one tile at a time (leftover i -> rank (F + i) %
 nranks, F = whole blocks).  A rank's k-th tile: its blocks' tiles first
@@ -36,12 +36,12 @@ def deal_block():
 
 
 def deal_weight(nranks):
-    """(m, V) of the weighted deal (vrt_internal.h VRT_DEAL_WEIGHT): from 4
+    """(m, V) of the weighted deal (vrt_internal.h VRT_DEAL_WEIGHT): from 2
     ranks on, rank 0 -- which also gathers and re-assembles the frame -- gets
     (m-1)/m of another rank's blocks, m = max(2, 48 // nranks); the whole
     blocks run in periods of V = m*nranks - 1 turns, position p of a period
     going to rank nranks-1 - p % nranks.  (0, 0): plain round robin."""
-    if nranks < 4:
+    if nranks < 2:
         return 0, 0
     m = max(2, 48 // nranks)
     return m, m * nranks - 1
