@@ -276,7 +276,7 @@ def trace_ab(a, libs, scenes, film):
                 for _ in range(4):
                     rc = L.vrt_trace_frame_device(h, C.byref(light), C.byref(lfilm), C.byref(view), C.byref(film),
                                                   0.0, 0, 1, 1, C.c_void_p(imgs[vi].data_ptr()),
-                                                  C.c_void_p(st.cuda_stream), C.byref(hits))
+                                                  C.c_void_p(st.cuda_stream), None)
                     assert rc == 0, L.vrt_last_error()
                 torch.cuda.synchronize()
                 if r > 0:

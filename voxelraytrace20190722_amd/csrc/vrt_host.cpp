@@ -22,6 +22,7 @@
 #include <cstring>
 #include <functional>
 #include <memory>
+#include <limits>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -329,8 +330,9 @@ struct HostOut {
 // One set of the full trace's scene scratch (vrt_scene::ts).
 struct TraceSet {
         LMRec *lm = nullptr;  // nodes x (LMRec + float4 cone record) + the finiteness flag
-        void *rec = nullptr;  // split-trace records (64 B per sample)
+        void *rec = nullptr;  // split-trace records (64 B per sample), the cone step table
         size_t rec_bytes = 0;
+        float steps_key[2] = { -1.f, -1.f };  // (mindist, maxdist) the step table holds
         hipEvent_t ev = nullptr;  // its last user's work
         bool live = false;
 };
@@ -1470,11 +1472,49 @@ static int ts_release(vrt_scene *s, int i, hipStream_t st)
 }
 
 // set i's light-map block (nodes x (LMRec + float4) + the flag word)
+// Per node, the cell a cone march's descent to it implies (TraceParams::
+// cells): the root's is all of space; a child's is its parent's cut at the
+// parent's box centre (AABB3D::center, as k_lm_aux computes it) on the side
+// of the child's octant -- per axis the tightest (lo, hi] the descent's
+// `pt > centre` choices establish.
+static std::vector<float4> cone_cells(const std::vector<NodeRec> &nodes)
+{
+        const float inf = std::numeric_limits<float>::infinity();
+        std::vector<float4> c(2 * nodes.size());
+        if (nodes.empty())
+                return c;
+        c[0] = make_float4(-inf, -inf, -inf, 0.f);
+        c[1] = make_float4(inf, inf, inf, 0.f);
+        for (size_t i = 0; i < nodes.size(); ++i) {  // BFS order: parents first
+                const NodeRec &nr = nodes[i];
+                if (nr.a & kLeafBit)
+                        continue;
+                const float cx = (nr.bmin[0] + nr.bmax[0]) * .5f, cy = (nr.bmin[1] + nr.bmax[1]) * .5f,
+                            cz = (nr.bmin[2] + nr.bmax[2]) * .5f;
+                for (uint32_t o = 0; o < 8; ++o) {
+                        float4 lo = c[2 * i], hi = c[2 * i + 1];
+                        if (o & 4) lo.x = std::max(lo.x, cx); else hi.x = std::min(hi.x, cx);
+                        if (o & 2) lo.y = std::max(lo.y, cy); else hi.y = std::min(hi.y, cy);
+                        if (o & 1) lo.z = std::max(lo.z, cz); else hi.z = std::min(hi.z, cz);
+                        c[2 * (size_t)(nr.a + o)] = lo;
+                        c[2 * (size_t)(nr.a + o) + 1] = hi;
+                }
+        }
+        return c;
+}
+
+// Trace set i's block: light map, cone-descent records, finiteness flag
+// (256 B), then the nodes' cone cells (static, filled on allocation).
 static int ensure_lm(vrt_scene *s, int i)
 {
-        if (!s->ts[i].lm)
+        if (!s->ts[i].lm) {
+                const size_t n = s->nodes.size();
                 HIPCHK(hipMalloc(reinterpret_cast<void **>(&s->ts[i].lm),
-                                 s->nodes.size() * (sizeof(LMRec) + sizeof(float4)) + 256));
+                                 n * (sizeof(LMRec) + sizeof(float4)) + 256 + n * 2 * sizeof(float4)));
+                const std::vector<float4> cells = cone_cells(s->nodes);
+                HIPCHK(hipMemcpy(reinterpret_cast<char *>(s->ts[i].lm) + n * (sizeof(LMRec) + sizeof(float4)) + 256,
+                                 cells.data(), cells.size() * sizeof(float4), hipMemcpyHostToDevice));
+        }
         return VRT_OK;
 }
 
@@ -1998,11 +2038,9 @@ static int lightmap_enqueue(vrt_scene *s, int set, const vrt_camera *light_cam, 
         uint32_t *d_bad = reinterpret_cast<uint32_t *>(d_cc + nnodes);
         if (int rc = ts_acquire(s, set, s->stream))  // a trace render may still read this set
                 return rc;
-        HIPCHK(hipMemsetAsync(d_lm, 0, (size_t)nnodes * sizeof(LMRec), s->stream));
-        HIPCHK(hipMemsetAsync(d_bad, 0, 4, s->stream));
         // scratch (sized for every sample hitting): 64-bit keys and 32-bit
         // slots in + out, the per-hit (illum, normal) records and their copy
-        // in sorted order, the sort's temp
+        // in sorted order, the sort's temp, the counters, the leaf runs
         size_t sort_bytes = 0;
         int kbits = 1, lbits = 1;
         while (kbits < 40 && (ns - 1) >> kbits)
@@ -2023,12 +2061,12 @@ static int lightmap_enqueue(vrt_scene *s, int set, const vrt_camera *light_cam, 
         uint32_t *v_out = reinterpret_cast<uint32_t *>(base + 2 * b8 + b4);
         float *samp = reinterpret_cast<float *>(base + 2 * b8 + 2 * b4);
         void *temp = base + 2 * b8 + 2 * b4 + b24;
-        char *tail = base + 2 * b8 + 2 * b4 + b24 + align_up(sort_bytes);
-        unsigned int *d_count = reinterpret_cast<unsigned int *>(tail);
-        unsigned int *d_nseg = reinterpret_cast<unsigned int *>(tail + 64);
-        uint32_t *d_seg = reinterpret_cast<uint32_t *>(tail + 256);
-        uint32_t *d_seg_end = reinterpret_cast<uint32_t *>(tail + 256 + bseg);
-        HIPCHK(hipMemsetAsync(tail, 0, 256, s->stream));
+        char *ctr = base + 2 * b8 + 2 * b4 + b24 + align_up(sort_bytes);
+        unsigned int *d_count = reinterpret_cast<unsigned int *>(ctr);
+        unsigned int *d_nseg = reinterpret_cast<unsigned int *>(ctr + 64);
+        unsigned int *d_tail_n = reinterpret_cast<unsigned int *>(ctr + 128);
+        uint32_t *d_seg = reinterpret_cast<uint32_t *>(ctr + 256);
+        uint32_t *d_seg_end = reinterpret_cast<uint32_t *>(ctr + 256 + bseg);
         LightParams lp;
         std::memset(&lp, 0, sizeof lp);
         fill_render_params(s, light_cam, light_film, 0, 1, &lp.r);
@@ -2039,9 +2077,12 @@ static int lightmap_enqueue(vrt_scene *s, int set, const vrt_camera *light_cam, 
         lp.keys = k_in;
         lp.vals = v_in;
         lp.samp = samp;
-        lp.tail_n = reinterpret_cast<unsigned int *>(tail + 128);
+        lp.tail_n = d_tail_n;
         lp.tail = v_out;  // free until the sort
         HIPCHK(hipEventRecord(s->ev0, s->stream));
+        // cone_trace_init_filter's leaf case first: it also zeroes the
+        // counters the passes below add to (no memsets)
+        HIPCHK(launch_lm_leaves(s->dev.nodes, nnodes, d_lm, d_bad, d_count, d_tail_n, d_nseg, s->stream));
         HIPCHK(launch_light(lp, s->stream));
         if (overlap)
                 if (int rc = overlap())
@@ -2067,7 +2108,7 @@ static int lightmap_enqueue(vrt_scene *s, int set, const vrt_camera *light_cam, 
 #ifdef VRT_LIGHT_TAIL_REPORT
         {
                 unsigned int ntail = 0;
-                HIPCHK(hipMemcpy(&ntail, lp.tail_n, sizeof ntail, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(&ntail, d_tail_n, sizeof ntail, hipMemcpyDeviceToHost));
                 std::fprintf(stderr, "light pass: %u of %lld samples deferred, %u hits\n", ntail, (long long)ns, nhit);
         }
 #endif
@@ -2075,8 +2116,7 @@ static int lightmap_enqueue(vrt_scene *s, int set, const vrt_camera *light_cam, 
                 HIPCHK(sort_pairs_u64(temp, &sort_bytes, k_in, k_out, v_in, v_out, nhit, kbits + lbits, s->stream));
         HIPCHK(launch_lm_accum(nhit, k_out, v_out, kbits, samp, d_seg, d_nseg, max_seg, d_seg_end, d_lm,
                                s->stream));
-        // cone_trace_init_filter: leaves, then internal levels bottom-up
-        HIPCHK(launch_lm_leaves(s->dev.nodes, nnodes, d_lm, s->stream));
+        // cone_trace_init_filter: internal levels bottom-up
         const int nlev = (int)s->level_begin.size() - 1;
         for (int l = nlev; l >= 1; --l)
                 HIPCHK(launch_lm_level(s->dev.nodes, s->level_begin[l - 1], s->level_begin[l], d_lm, s->stream));
@@ -2161,8 +2201,11 @@ static int trace_scratch(vrt_scene *s, int set, const TraceParams &tp, TracePara
         *out = tp;
         TraceSet &t = s->ts[set];
         const size_t nslots = (size_t)tp.r.tiles_this_rank * 256;
-        // the primary pass's 64-B records, its deferred-sample count and list
-        const size_t need = nslots * 64 + 512 + nslots * 4;
+        // the cone step table and its length (at fixed offsets: the table
+        // outlives calls with other tile counts), the primary pass's 64-B
+        // records, its deferred-sample count (512 B) and list
+        const size_t head = (size_t)kConeSteps * 16 + 256;
+        const size_t need = head + nslots * 64 + 512 + nslots * 4;
         if (t.rec_bytes < need) {
                 if (t.rec) {
                         HIPCHK(hipDeviceSynchronize());  // callers may have queued work on any stream
@@ -2172,10 +2215,19 @@ static int trace_scratch(vrt_scene *s, int set, const TraceParams &tp, TracePara
                 }
                 HIPCHK(hipMalloc(&t.rec, need));
                 t.rec_bytes = need;
+                t.steps_key[0] = t.steps_key[1] = -1.f;
         }
-        out->rec = reinterpret_cast<float4 *>(t.rec);
-        out->tail_n = reinterpret_cast<unsigned int *>(static_cast<char *>(t.rec) + nslots * 64);
-        out->tail = reinterpret_cast<uint32_t *>(static_cast<char *>(t.rec) + nslots * 64 + 512);
+        // the step table depends on mindist and maxdist only: rebuilt when
+        // they change (the set's users are ordered by its event)
+        out->build_steps = !(t.steps_key[0] == tp.mindist && t.steps_key[1] == tp.maxdist);
+        t.steps_key[0] = tp.mindist;
+        t.steps_key[1] = tp.maxdist;
+        char *b = static_cast<char *>(t.rec);
+        out->steps = reinterpret_cast<float4 *>(b);
+        out->nsteps = reinterpret_cast<int *>(b + (size_t)kConeSteps * 16);
+        out->rec = reinterpret_cast<float4 *>(b + head);
+        out->tail_n = reinterpret_cast<unsigned int *>(b + head + nslots * 64);
+        out->tail = reinterpret_cast<uint32_t *>(b + head + nslots * 64 + 512);
         return VRT_OK;
 }
 
@@ -2241,6 +2293,7 @@ static void fill_trace_params(vrt_scene *s, int set, const vrt_camera *cam, cons
         tp->lm = s->ts[set].lm;
         tp->cc = reinterpret_cast<const float4 *>(s->ts[set].lm + s->nodes.size());
         tp->lm_bad = reinterpret_cast<const uint32_t *>(tp->cc + s->nodes.size());
+        tp->cells = reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(tp->lm_bad) + 256);
         // float mindist = 1.414f * min_voxel_size; maxdist = length(root.aabb.size())
         tp->mindist = 1.414f * min_voxel;
         const f3 sz = mk3(s->info.root_max[0] - s->info.root_min[0], s->info.root_max[1] - s->info.root_min[1],

@@ -442,6 +442,7 @@ struct TraceParams {
         const LMRec *lm;
         const float4 *cc;          // per node: box centre xyz, word a (cone descent)
         const uint32_t *lm_bad;    // != 0: some illum is not finite (exact slow path)
+        const float4 *cells;       // per node: the cell (lo.xyz, hi.xyz) of the descent to it
         float mindist, maxdist;
         float split_up[64];
         // split_bound[k] (k = 1..63) = the largest cone diameter whose split
@@ -457,7 +458,17 @@ struct TraceParams {
         // the primary pass's deferred samples (k_trace_prim_tail): count, slots
         unsigned int *tail_n;
         uint32_t *tail;
+        // the cone march's step table (kConeSteps entries) and its length,
+        // written by k_cone_steps (launched after k_trace_prim)
+        float4 *steps;
+        int *nsteps;
+        int32_t build_steps;  // launch_trace_prim rebuilds the table (k_cone_steps)
 };
+// Capacity of TraceParams::steps.  A cone's distance grows by >= 11.5 % a
+// step (diam >= 2 * aperture * dist), so even maxdist / mindist = 2^128
+// takes < 820 steps; a longer sequence (not reachable for finite scenes)
+// is flagged (-1) and the march computes its steps inline.
+constexpr int kConeSteps = 1024;
 
 // GPU octree build (vrt_build.hip): the host build's
 // arrays, produced on `device` and copied back.
@@ -520,12 +531,17 @@ bool build_flag(const char *name, int64_t *value);
 hipError_t launch_light(const LightParams &p, hipStream_t st);
 hipError_t light_diag_copy(void *host, size_t bytes);  // VRT_LIGHT_DIAG builds
 // samp: n x 6 floats followed by room for their sorted copy (n x 6);
-// seg_start: max_seg entries (>= non-empty leaves), nseg zeroed; seg_end:
-// one entry per node (each hit leaf's run end is written)
+// seg_start: max_seg entries (>= non-empty leaves), nseg zeroed (by
+// launch_lm_leaves); seg_end: one entry per node (each hit leaf's run end is
+// written)
 hipError_t launch_lm_accum(int64_t n, const uint64_t *keys_sorted, const uint32_t *vals_sorted, int kbits,
                            const float *samp, uint32_t *seg_start, unsigned int *nseg,
                            int64_t max_seg, uint32_t *seg_end, LMRec *lm, hipStream_t st);
-hipError_t launch_lm_leaves(const NodeRec *nodes, int64_t nnodes, LMRec *lm, hipStream_t st);
+// every leaf's coverage and (zero) illum; also zeroes the light map's
+// counters (the finiteness flag, the hit, deferred-sample and run counts) --
+// the first kernel of a light-map build, so nothing is cleared by a memset
+hipError_t launch_lm_leaves(const NodeRec *nodes, int64_t nnodes, LMRec *lm, uint32_t *bad, unsigned int *count,
+                            unsigned int *tail_n, unsigned int *nseg, hipStream_t st);
 hipError_t launch_lm_level(const NodeRec *nodes, int64_t begin, int64_t end, LMRec *lm, hipStream_t st);
 hipError_t launch_trace(const TraceParams &p, hipStream_t st);
 hipError_t launch_trace_prim(const TraceParams &p, hipStream_t st);

@@ -3575,24 +3575,30 @@ __global__ __launch_bounds__(256) void k_lm_accum(const float *__restrict__ samp
         lm[leaf].illum[l] = acc;
 }
 
-// cone_trace_init_filter, leaf case (VRT/voxel_octree.cc:192-200)
+// cone_trace_init_filter, leaf case (VRT/voxel_octree.cc:192-200), run
+// first: every leaf's illum starts at zero (k_lm_accum then writes the sums
+// of the leaves with hits; an empty leaf has none) and its coverage is set.
+// Block 0 also zeroes the build's counters.
 __global__ __launch_bounds__(256) void k_lm_leaves(const NodeRec *__restrict__ nodes, int64_t n,
-                                                   LMRec *__restrict__ lm)
+                                                   LMRec *__restrict__ lm, uint32_t *bad, unsigned int *count,
+                                                   unsigned int *tail_n, unsigned int *nseg)
 {
         const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i == 0) {
+                *bad = 0u;
+                *count = 0u;
+                *tail_n = 0u;
+                *nseg = 0u;
+        }
         if (i >= n)
                 return;
         const uint32_t a = nodes[i].a;
         if (!(a & kLeafBit))
                 return;
-        if ((a & ~kLeafBit) == 0) {
-                lm[i].cov = 0.f;
+        lm[i].cov = (a & ~kLeafBit) == 0 ? 0.f : 1.f;
 #pragma unroll
-                for (int f = 0; f < 18; ++f)
-                        lm[i].illum[f] = 0.f;
-        } else {
-                lm[i].cov = 1.f;
-        }
+        for (int f = 0; f < 18; ++f)
+                lm[i].illum[f] = 0.f;
 }
 
 // cone_trace_init_filter, internal case for one BFS level (children in
@@ -3762,41 +3768,41 @@ __device__ __forceinline__ int octant_of(const f3 &pt, const float4 &c)
 // The descent also records the cell of the point it followed -- per
 // axis the half-open interval (lo, hi] cut by the centres whose octant
 // choice it used (pt > centre: lo, else hi; the octree's cells are nested,
-// max/min keep the tightest) -- and the next step at the same split level
+// max/min keep the tightest), a property of the node reached, read from
+// TraceParams::cells -- and the next step at the same split level
 // whose point lies in that cell makes the same choices at every node of the
 // path, so it reuses the node (and whether the descent ended above the split
 // level) without descending.  Any other step descends from the root.
-__device__ __forceinline__ f3 cone_march_axes(const TraceParams &p, f3 o, f3 d, const float co[6])
+//
+// The steps come from the cone step table (k_cone_steps): a step's
+// distance, split level and distance weight depend on mindist and maxdist
+// only, not on the cone, so they are computed once per frame and read here
+// with scalar loads; the cone ends at the table's end or at opacity 1, where
+// the reference's loop ends.
+__device__ __forceinline__ f3 cone_march_axes(const TraceParams &p, f3 o, f3 d, const float co[6], int nsteps)
 {
-        const float aperture = 0.577350269f, step = .1f, decay = 1.f;
+        const float step = .1f;
         const int jx = co[0] != 0.f ? 0 : 3, jy = co[1] != 0.f ? 1 : 4, jz = co[2] != 0.f ? 2 : 5;
         const float cx = co[jx], cy = co[jy], cz = co[jz];
         const float4 c0 = p.cc[0];
         const uint32_t a0 = __float_as_uint(c0.w);
-        float dist = p.mindist;
         float opacity = 0.f;
         f3 diffuse = mk3(0.f, 0.f, 0.f);
-        int level = -1;
-        float bound = 0.f;
         // the last descent's cell
         f3 lo = mk3(0.f, 0.f, 0.f), hi = lo;
         int c_level = -1, c_split = 0;
         uint32_t c_ni = 0;
         float cov = 0.f;
         f3 il = mk3(0.f, 0.f, 0.f);
-        for (int guard = 0; dist < p.maxdist && opacity < 1.f && guard < (1 << 16); ++guard) {
+        // (constant address space, index the same in every active lane: the
+        // entries are scalar loads)
+        typedef const __attribute__((address_space(4))) float ConstF;
+        ConstF *tab = (ConstF *)p.steps;
+        for (int k = 0; k < nsteps && opacity < 1.f; ++k) {
+                const int ku = __builtin_amdgcn_readfirstlane(k) * 4;
+                const float dist = tab[ku], inv = tab[ku + 1];
+                const int level = __float_as_int(tab[ku + 2]);
                 const f3 pt = o + d * dist;
-                const float diam = std_max(p.mindist, aperture * 2.f * dist);
-                if (p.maxdist < diam)
-                        break;
-                if (level < 0) {
-                        level = min(split_level_of(p.maxdist / diam, p.split_up), 63);
-                        bound = p.split_bound[level];
-                }
-                while (level > 0 && diam > bound) {
-                        --level;
-                        bound = p.split_bound[level];
-                }
                 int split = level;
                 uint32_t ni = 0;
                 bool same = false;
@@ -3809,18 +3815,17 @@ __device__ __forceinline__ f3 cone_march_axes(const TraceParams &p, f3 o, f3 d, 
                         uint32_t a = a0;
                         float4 c = c0;
                         int i = octant_of(pt, c0);
-                        lo = mk3(-__builtin_inff(), -__builtin_inff(), -__builtin_inff());
-                        hi = mk3(__builtin_inff(), __builtin_inff(), __builtin_inff());
                         while (!(a & kLeafBit) && split) {
-                                if (i & 4) lo.x = std::max(lo.x, c.x); else hi.x = std::min(hi.x, c.x);
-                                if (i & 2) lo.y = std::max(lo.y, c.y); else hi.y = std::min(hi.y, c.y);
-                                if (i & 1) lo.z = std::max(lo.z, c.z); else hi.z = std::min(hi.z, c.z);
                                 ni = a + (uint32_t)i;
                                 c = p.cc[ni];
                                 a = __float_as_uint(c.w);
                                 i = octant_of(pt, c);
                                 split--;
                         }
+                        // the cell of the path (precomputed per node: cone_cells)
+                        const float4 l4 = p.cells[2 * ni], h4 = p.cells[2 * ni + 1];
+                        lo = mk3(l4.x, l4.y, l4.z);
+                        hi = mk3(h4.x, h4.y, h4.z);
                         c_level = level;
                         c_split = split;
                         c_ni = ni;
@@ -3856,14 +3861,49 @@ __device__ __forceinline__ f3 cone_march_axes(const TraceParams &p, f3 o, f3 d, 
                         if (cov != 0.f) {
                                 const float transparency = clampf(1.f - opacity, 0.f, 1.f);
                                 const float aa = cov * step;
-                                const float w = (1.f / (1.f + decay * dist)) * transparency * cov;
+                                const float w = inv * transparency * cov;  // inv = 1 / (1 + decay * dist)
                                 diffuse = mk3(diffuse.x + w * il.x, diffuse.y + w * il.y, diffuse.z + w * il.z);
                                 opacity += transparency * aa;
                         }
                 }
-                dist += step * diam;
         }
         return diffuse;
+}
+
+// The cone march's step sequence (cone_trace's loop, VRT/voxel_octree.cc:
+// 276-311, with the split level kept by the split_bound cursor): per step
+// (dist, 1 / (1 + decay * dist), split level, diam), the same operations as
+// cone_march_fast's loop header, up to the step where dist reaches maxdist
+// or maxdist < diam.  -1 if longer than kConeSteps.  One lane, launched
+// after k_trace_prim (k_cones_film follows on the stream).
+__global__ __launch_bounds__(64) void k_cone_steps(TraceParams p)
+{
+        if (threadIdx.x != 0)
+                return;
+        const float aperture = 0.577350269f, step = .1f, decay = 1.f;
+        float dist = p.mindist;
+        int level = -1, n = 0;
+        float bound = 0.f;
+        for (int guard = 0; dist < p.maxdist && guard < (1 << 16); ++guard) {
+                const float diam = std_max(p.mindist, aperture * 2.f * dist);
+                if (p.maxdist < diam)
+                        break;
+                if (level < 0) {
+                        level = min(split_level_of(p.maxdist / diam, p.split_up), 63);
+                        bound = p.split_bound[level];
+                }
+                while (level > 0 && diam > bound) {
+                        --level;
+                        bound = p.split_bound[level];
+                }
+                if (n == kConeSteps) {
+                        n = -1;
+                        break;
+                }
+                p.steps[n++] = make_float4(dist, 1.f / (1.f + decay * dist), __int_as_float(level), diam);
+                dist += step * diam;
+        }
+        *p.nsteps = n;
 }
 
 // cone_trace(root, cone, min_voxel_size) (VRT/voxel_octree.cc:276-311)
@@ -3879,9 +3919,10 @@ __device__ __forceinline__ f3 cone_march(const TraceParams &p, f3 o, f3 d)
                         co[i] = clampf(dot(illum_dir(i), nd), 0.f, 1.f);
                 const bool twin = (co[0] != 0.f && co[3] != 0.f) || (co[1] != 0.f && co[4] != 0.f) ||
                                   (co[2] != 0.f && co[5] != 0.f);
-                if (!twin)
-                        return cone_march_axes(p, o, d, co);
-                return cone_march_fast(p, o, d);  // a NaN direction
+                const int nsteps = *p.nsteps;
+                if (!twin && nsteps >= 0 && nsteps <= kConeSteps)
+                        return cone_march_axes(p, o, d, co, nsteps);
+                return cone_march_fast(p, o, d);  // a NaN direction (or no step table)
         }
         return cone_march_ref(p, o, d);
 }
@@ -4077,7 +4118,7 @@ __global__ __launch_bounds__(64) void k_trace_prim_tail(TraceParams p)
 // pixel is written once: each sample record is read once, and no per-cone
 // result goes through memory.
 #ifndef VRT_CONES_WAVES_PER_EU
-#define VRT_CONES_WAVES_PER_EU 7  // 70 VGPRs, no spill: +9.8 % over 8 waves (64 VGPRs, 36 B/lane of spill once the direct term moved here; round 4)
+#define VRT_CONES_WAVES_PER_EU 8  // 64 VGPRs, 24 B/lane of spill: +1.9 % over 7 waves (70 VGPRs) since the step table and cells (round 5; round 4, before them: 7 waves +9.8 %)
 #endif
 __global__ __launch_bounds__(64, VRT_CONES_WAVES_PER_EU) void k_cones_film(TraceParams p)
 {
@@ -4181,11 +4222,11 @@ hipError_t launch_lm_accum(int64_t n, const uint64_t *keys_sorted, const uint32_
         return hipGetLastError();
 }
 
-hipError_t launch_lm_leaves(const NodeRec *nodes, int64_t nnodes, LMRec *lm, hipStream_t st)
+hipError_t launch_lm_leaves(const NodeRec *nodes, int64_t nnodes, LMRec *lm, uint32_t *bad, unsigned int *count,
+                            unsigned int *tail_n, unsigned int *nseg, hipStream_t st)
 {
-        if (nnodes <= 0)
-                return hipSuccess;
-        hipLaunchKernelGGL(k_lm_leaves, dim3((unsigned)((nnodes + 255) / 256)), dim3(256), 0, st, nodes, nnodes, lm);
+        const unsigned g = (unsigned)std::max<int64_t>(1, (nnodes + 255) / 256);
+        hipLaunchKernelGGL(k_lm_leaves, dim3(g), dim3(256), 0, st, nodes, nnodes, lm, bad, count, tail_n, nseg);
         return hipGetLastError();
 }
 
@@ -4222,6 +4263,8 @@ hipError_t launch_trace_prim(const TraceParams &p, hipStream_t st)
         if (tail)
                 hipLaunchKernelGGL(p.r.sc.wide_leaves ? k_trace_prim_tail<true> : k_trace_prim_tail<false>,
                                    dim3(VRT_LIGHT_TAIL_GRID), dim3(64), 0, st, p);
+        if (p.build_steps)
+                hipLaunchKernelGGL(k_cone_steps, dim3(1), dim3(64), 0, st, p);
         return hipGetLastError();
 }
 
