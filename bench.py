@@ -402,6 +402,9 @@ def parse():
                    help="with --rehearse-ranks: whose share to render (0: rank 0, which also gathers and "
                         "unpacks; from 4 ranks on the deal gives it fewer tiles than the others; -1 (default): "
                         "every rank's in turn, the reported step = the slowest rank's)")
+    p.add_argument("--rehearse-repeats", type=int, default=3,
+                   help="with --rehearse-ranks: timed runs per rank's share, interleaved over the ranks; a rank's "
+                        "step is the median of its runs (all printed in rehearsal.per_rank)")
     p.add_argument("--rehearse-render-only", action="store_true",
                    help="with --rehearse-ranks: time the share's renders alone (no gather, no unpack)")
     p.add_argument("--frames-in-flight-trace", type=int, default=1,
@@ -836,18 +839,29 @@ def main():
     reh_rows = []
     if rehearse:
         order = list(range(nshare)) if a.rehearse_rank < 0 else [a.rehearse_rank]
+        # every rank's share timed --rehearse-repeats times, the repeats
+        # interleaved over the ranks (a momentary slowdown of the box lands
+        # on one repeat of one rank, not on one rank's only run); a rank's
+        # step = the median of its repeats, all of them printed
+        reps = {r_: [] for r_ in order}
+        for rep_ in range(max(1, a.rehearse_repeats)):
+            for r_ in order:
+                cur["share"] = r_
+                el_, ell_, he_ = timed_run()
+                kms_ = np.array([s.elapsed_time(e) for s, e in ev])
+                coll_ = float(np.mean([ev[k][1].elapsed_time(ev_coll[k]) for k in coll_done])) if coll_done else 0.0
+                unp_ = float(np.mean([ev_unp[k][0].elapsed_time(ev_unp[k][1]) for k in unp_done])) if unp_done else 0.0
+                reps[r_].append((el_, ell_, he_, kms_, coll_, unp_))
+                log(f"[rehearsal] rank {r_}'s share, repeat {rep_}: {el_ * 1e3 / a.steps:.4f} ms per step")
         runs = []
         for r_ in order:
-            cur["share"] = r_
-            el_, ell_, he_ = timed_run()
-            kms_ = np.array([s.elapsed_time(e) for s, e in ev])
-            coll_ = float(np.mean([ev[k][1].elapsed_time(ev_coll[k]) for k in coll_done])) if coll_done else 0.0
-            unp_ = float(np.mean([ev_unp[k][0].elapsed_time(ev_unp[k][1]) for k in unp_done])) if unp_done else 0.0
+            rr = sorted(reps[r_], key=lambda x: x[0])
+            el_, ell_, he_, kms_, coll_, unp_ = rr[(len(rr) - 1) // 2]  # the median run (lower median)
             runs.append((el_, ell_, he_, kms_, coll_, unp_))
             reh_rows.append({"share_of_rank": r_, "ms_per_step": round(el_ * 1e3 / a.steps, 4),
+                             "repeats_ms_per_step": [round(x[0] * 1e3 / a.steps, 4) for x in reps[r_]],
                              "share_render_ms": round(float(kms_.mean()), 4), "collective_ms": round(coll_, 4),
                              "unpack_ms": round(unp_, 4), "host_enqueue_ms_per_step": round(he_ * 1e3 / a.steps, 4)})
-            log(f"[rehearsal] rank {r_}'s share: {el_ * 1e3 / a.steps:.4f} ms per step")
         worst = max(range(len(runs)), key=lambda i: runs[i][0])
         elapsed, elapsed_local, host_enq, kms_w, _, _ = runs[worst]
         cur["share"] = order[worst]
@@ -1250,7 +1264,8 @@ def main():
             out["rehearsal"] = {
                 "ranks": nshare, "share_of_rank": cur["share"],
                 "shares_rehearsed": [r_["share_of_rank"] for r_ in reh_rows],
-                "step_is": "max over the rehearsed ranks' steps" if len(reh_rows) > 1 else "the one rehearsed rank's step",
+                "step_is": ("max over the rehearsed ranks' steps" if len(reh_rows) > 1 else "the one rehearsed rank's step")
+                + f" (each rank's step: the median of its {max(1, a.rehearse_repeats)} interleaved timed runs)",
                 "per_rank": reh_rows,
                 "frames_per_s": round(a.steps / elapsed, 2),
                 "projected_Mrays_per_s_without_xgmi": round(value, 2),
