@@ -514,6 +514,24 @@ def test_lightmap_and_trace_match_oracle(proxy_small, depth, light_n):
         assert np.array_equal(bits(rgb), bits(orgb))
 
 
+def test_trace_step_table_follows_min_voxel_and_film(proxy_small):
+    """The cone step table (k_cone_steps) is kept per trace set and rebuilt
+    only when (mindist, maxdist) change: renders alternating the cone step
+    (min_voxel) and the film size (the records move, the table stays at its
+    fixed offset) each match the oracle bit for bit."""
+    tree = vrt.VoxelOctree(proxy_small, 6)
+    osc = po.Scene(proxy_small, 6)
+    tree.lightmap(vrt.Camera(*LIGHT), vrt.Film(1, 1, 96, 96))
+    osc.lightmap(po.camera(*LIGHT), 1.0, 1.0, 96, 96, nthreads=8)
+    res = tree.min_voxel(6)
+    view = (vrt.to_radian(90), (1.0, 1.3, -0.2), (0.0, 0.4, 0.0), (0.0, 1.0, 0.0))
+    for mv, (nx, ny) in [(res, (40, 32)), (2.0 * res, (40, 32)), (res, (48, 40)), (res, (40, 32)),
+                         (0.5 * res, (48, 40))]:
+        rgb = tree.render_trace(vrt.Camera(*view), vrt.Film(1, 1, nx, ny), mv)
+        orgb, _ = osc.render_trace(po.camera(*view), 1.0, 1.0, nx, ny, mv, nthreads=8)
+        assert np.array_equal(bits(rgb), bits(orgb)), (mv, nx, ny)
+
+
 @pytest.mark.parametrize("depth,light_n", [(5, 96), (8, 128)])
 def test_lightmap_tail_walk_matches_oracle(proxy_small, depth, light_n):
     """The light pass's tail launch (k_light_tail: one sample per wave, the
