@@ -211,8 +211,9 @@ def test_c5_frames_in_flight_match_oracle(proxy, flags):
     without a host sync (one primary-record / visibility buffer pair per
     stream), the film changing from 640x360 to 1280x720 partway (per-frame
     scratch sized anew) -- every visibility image equals the oracle's.
-    flags=TEST_SPILL_ALL: in a compaction build (VRT_SEC_COOP=0) nearly every
-    ray is saved and resumed, through the scene's alternating scratch sets."""
+    flags=TEST_SPILL_ALL: nearly every ray is saved and resumed (the
+    compaction is the default build's path: vrt_build_flag), through the
+    scene's alternating scratch sets."""
     import torch
     tree, osc = scenes(proxy, 8)
     mn, mx = tree.root_box

@@ -1,4 +1,4 @@
-"""The leaf triangle-box skip of the fast march (DevScene::mnodes,
+"""The leaf triangle-box skip of the fast march (DevScene::xnodes,
 vrt_host.cpp march_nodes, vrt_kernels.hip line_meets_box) must never skip a
 leaf that holds a triangle intersect_triangle3 accepts.  Certificate test on
 the CPU: adversarial rays aimed at triangle edges and vertices (where the
