@@ -3382,7 +3382,11 @@ __device__ __forceinline__ bool tile_lane(const RenderParams &p, int u, int &k, 
 // waves of samples landing in the large leaves under dense geometry (up to
 // ~2000 serial triangle tests per lane).
 #ifndef VRT_LIGHT_BUDGET
-#define VRT_LIGHT_BUDGET 256
+// 768 since round 5: the light map alone builds faster at 256 (round 4's
+// choice), but in the whole frame, where the tail runs beside the view's
+// primary march, 256 / 512 / 768 / 1,024 / 2,048 give 4.013 / 3.973 / 3.965 /
+// 3.962 / 4.17 ms per frame
+#define VRT_LIGHT_BUDGET 768
 #endif
 #ifndef VRT_LIGHT_TAIL_GRID
 #define VRT_LIGHT_TAIL_GRID 8192
