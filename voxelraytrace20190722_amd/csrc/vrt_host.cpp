@@ -1331,7 +1331,9 @@ static int ts_release(vrt_scene *s, int i, hipStream_t st);
 // compaction) when the build disables it, the film has 2^26 pixels or more,
 // the octree 2^24 nodes or more (SpillRec's packed words), or the allocation
 // fails.
-constexpr uint32_t kSpillCapMax = (uint32_t)((size_t)1 << 30) / (kSpillChunk * (uint32_t)sizeof(SpillRec));  // chunks
+// chunks: the records, their two fill words and the counters within 1 GiB
+constexpr uint32_t kSpillCapMax =
+        (uint32_t)((((size_t)1 << 30) - 4096) / ((size_t)kSpillChunk * sizeof(SpillRec) + 8));
 static int spill_setup(vrt_scene *s, int64_t rays, int64_t pixels, hipStream_t st, SpillQueues *sq, int *set)
 {
         *sq = spill_defaults();

@@ -2727,7 +2727,11 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
 }
 
 #ifndef VRT_SEC_SPILL_T
-#define VRT_SEC_SPILL_T 12    // phase A stops below this many walking lanes (0: no compaction); round 4 with the streaming resume: 8 / 12 / 16 / 20 / 24 / 32 / 48 = 18.07 / 17.21 / 17.28 / 17.54 / 17.65 / 17.66 / 17.83 ms
+// phase A stops below this many walking lanes (0: no compaction).  Round 5
+// (64-B packed records): 8 / 12 / 14 / 16 / 18 / 20 / 24 = 18.11 / 17.21 /
+// 16.96 / 16.81 / 16.75 / 16.81 / 16.93 ms per frame (round 4, 128-B records:
+// 12 was best, 17.21 vs 17.28 at 16)
+#define VRT_SEC_SPILL_T 18
 #endif
 static_assert(kSpillStack >= kStack, "SpillRec stack");
 
