@@ -291,6 +291,12 @@ int vrt_test_flags(void);
  * used) by the scene's last config-5 launch; waits for it.  All 0 when that
  * launch used no compaction. */
 int vrt_secondary_spill_counts(vrt_scene *s, int64_t counts[4]);
+/* Diagnostic: the scene's last config-5 launch's compaction, waits for it:
+ * stats[0] records queued, [1] stopped rays finished in place because the
+ * queue was full, [2] queue chunks taken, [3] chunks allocated, [4] chunks
+ * left to the batch-pool launch after the streaming round, [5] bytes per
+ * record.  All 0 when that launch used no compaction. */
+int vrt_secondary_spill_stats(vrt_scene *s, int64_t stats[6]);
 /* Device bytes the scene holds beyond its octree, triangles and textures
  * (vrt_scene_info().device_bytes): per-call scratch kept between calls --
  * config 5's compaction queues (*spill_bytes, may be NULL), the light-map

@@ -532,6 +532,34 @@ def test_trace_step_table_follows_min_voxel_and_film(proxy_small):
         assert np.array_equal(bits(rgb), bits(orgb)), (mv, nx, ny)
 
 
+def test_trace_step_table_survives_failed_frame(proxy_small):
+    """A frame that fails after its trace set's scratch is set up (here: a
+    light film too large for the light pass, rejected before any kernel
+    runs) must not mark the set's cone step table as built: the next frames
+    on both sets (trace frames alternate the scene's two sets) with the same
+    min_voxel match the oracle (the key used to be committed
+    before k_cone_steps was enqueued)."""
+    import torch
+    tree = vrt.VoxelOctree(proxy_small, 6)
+    osc = po.Scene(proxy_small, 6)
+    res = tree.min_voxel(6)
+    view = (vrt.to_radian(90), (1.0, 1.3, -0.2), (0.0, 0.4, 0.0), (0.0, 1.0, 0.0))
+    film = vrt.Film(1, 1, 40, 32)
+    img = torch.zeros((32, 40, 3), device="cuda")
+    with pytest.raises(vrt.VrtError):
+        tree.trace_frame_device(vrt.Camera(*LIGHT), vrt.Film(1, 1, 32768, 32768), vrt.Camera(*view), film, 0, 1, 1,
+                                img.data_ptr(), res)
+    osc.lightmap(po.camera(*LIGHT), 1.0, 1.0, 96, 96, nthreads=8)
+    want, _ = osc.render_trace(po.camera(*view), 1.0, 1.0, 40, 32, res, nthreads=8)
+    for k in range(3):  # sets 1, 0, 1 after the failed frame took set 0
+        img.zero_()
+        tree.trace_frame_device(vrt.Camera(*LIGHT), vrt.Film(1, 1, 96, 96), vrt.Camera(*view), film, 0, 1, 1,
+                                img.data_ptr(), res)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(img.cpu().numpy()), bits(want)), k
+    assert np.array_equal(bits(tree.render_trace(vrt.Camera(*view), film, res)), bits(want))
+
+
 @pytest.mark.parametrize("depth,light_n", [(5, 96), (8, 128)])
 def test_lightmap_tail_walk_matches_oracle(proxy_small, depth, light_n):
     """The light pass's tail launch (k_light_tail: one sample per wave, the

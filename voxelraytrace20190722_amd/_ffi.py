@@ -126,6 +126,7 @@ SIGNATURES = {
     "vrt_set_test_flags": (C.c_int, [C.c_int]),
     "vrt_camera_defer_bound": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]),
     "vrt_secondary_spill_counts": (C.c_int, [_P, i64p]),
+    "vrt_secondary_spill_stats": (C.c_int, [_P, i64p]),
     "vrt_scene_scratch_bytes": (C.c_int, [_P, i64p, i64p]),
     "vrt_device_selftest_order": (C.c_int, [C.c_int, f32p, u32p, C.c_int64, u32p, f32p, i32p, C.c_int64,
                                             C.c_int32, i32p]),

@@ -430,6 +430,15 @@ class VoxelOctree:
         check(lib().vrt_secondary_spill_counts(self.h, c), "vrt_secondary_spill_counts")
         return list(c)
 
+    def secondary_spill_stats(self):
+        """The last config-5 launch's compaction (vrt_secondary_spill_stats):
+        {records, finished_in_place, chunks_taken, chunks_allocated,
+        leftover_chunks, record_bytes}."""
+        c = (C.c_int64 * 6)()
+        check(lib().vrt_secondary_spill_stats(self.h, c), "vrt_secondary_spill_stats")
+        return dict(zip(("records", "finished_in_place", "chunks_taken", "chunks_allocated", "leftover_chunks",
+                         "record_bytes"), list(c)))
+
     def scratch_bytes(self):
         """(total, compaction) device bytes of scratch the scene keeps between
         calls (vrt_scene_scratch_bytes)."""

@@ -1268,9 +1268,7 @@ static int queue_take(vrt_scene *s, hipStream_t st, WorkQueue *q, int *slot)
 static int queue_release(vrt_scene *s, int slot, hipStream_t st, const int slice_units[8], int waves)
 {
         for (int x = 0; x < 8; ++x)
-                if (waves < 0)  // the launch's last wave zeroed the counters (k_render_p)
-                        s->q_base[slot][x] = 0;
-                else if (slice_units[x] > 0)
+                if (slice_units[x] > 0)
                         s->q_base[slot][x] += (uint32_t)slice_units[x] + (uint32_t)waves;
         HIPCHK(hipEventRecord(s->q_ev[slot], st));
         s->q_live[slot] = true;
@@ -1380,7 +1378,11 @@ static int spill_setup(vrt_scene *s, int64_t rays, int64_t pixels, hipStream_t s
         const size_t ctr_bytes = (size_t)kSpillMaxRounds * kSpillCtrStride * 4;
         if (s->spill_cap[k] < nch) {
                 if (s->d_spill[k]) {
-                        HIPCHK(hipDeviceSynchronize());  // earlier launches on any stream may use it
+                        // the set's users on any stream are ordered by its event
+                        // (spill_done after each, a stream wait when a set
+                        // changes stream): the last one's event covers them all
+                        if (s->spill_live[k])
+                                HIPCHK(hipEventSynchronize(s->spill_ev[k]));
                         (void)hipFree(s->d_spill[k]);
                         s->d_spill[k] = nullptr;
                         s->spill_cap[k] = 0;
@@ -1507,12 +1509,19 @@ static std::vector<float4> cone_cells(const std::vector<NodeRec> &nodes)
 
 // Trace set i's block: light map, cone-descent records, finiteness flag
 // (256 B), then the nodes' cone cells (static, filled on allocation).
+// One trace set's light-map block: the light map (LMRec per node), the
+// cone-descent records (float4 per node), the non-finite flag (256 B) and the
+// per-node cells (2 float4 per node)
+static size_t lm_set_bytes(size_t n)
+{
+        return n * (sizeof(LMRec) + sizeof(float4)) + 256 + n * 2 * sizeof(float4);
+}
+
 static int ensure_lm(vrt_scene *s, int i)
 {
         if (!s->ts[i].lm) {
                 const size_t n = s->nodes.size();
-                HIPCHK(hipMalloc(reinterpret_cast<void **>(&s->ts[i].lm),
-                                 n * (sizeof(LMRec) + sizeof(float4)) + 256 + n * 2 * sizeof(float4)));
+                HIPCHK(hipMalloc(reinterpret_cast<void **>(&s->ts[i].lm), lm_set_bytes(n)));
                 const std::vector<float4> cells = cone_cells(s->nodes);
                 HIPCHK(hipMemcpy(reinterpret_cast<char *>(s->ts[i].lm) + n * (sizeof(LMRec) + sizeof(float4)) + 256,
                                  cells.data(), cells.size() * sizeof(float4), hipMemcpyHostToDevice));
@@ -1871,7 +1880,7 @@ extern "C" int vrt_scene_scratch_bytes(vrt_scene *s, int64_t *bytes, int64_t *sp
         int64_t t = sp + (int64_t)s->light_bytes + (int64_t)s->ho.bytes;
         for (const TraceSet &ts : s->ts) {
                 if (ts.lm)
-                        t += (int64_t)s->nodes.size() * (int64_t)(sizeof(LMRec) + sizeof(float4)) + 256;
+                        t += (int64_t)lm_set_bytes(s->nodes.size());
                 t += (int64_t)ts.rec_bytes;
         }
         *bytes = t;
@@ -1892,11 +1901,35 @@ extern "C" int vrt_secondary_spill_counts(vrt_scene *s, int64_t counts[4])
         if (s->spill_last < 0 || !s->d_spill[s->spill_last])
                 return VRT_OK;
         HIPCHK(hipSetDevice(s->device));
-        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipEventSynchronize(s->spill_ev[s->spill_last]));  // the set's last launch
         std::vector<uint32_t> c((size_t)kSpillMaxRounds * kSpillCtrStride);
         HIPCHK(hipMemcpy(c.data(), s->d_spill[s->spill_last], c.size() * 4, hipMemcpyDeviceToHost));
         for (int r = 0; r < 4 && r < kSpillMaxRounds; ++r)
                 counts[r] = c[(size_t)r * kSpillCtrStride + 2];  // records (spill_close)
+        return VRT_OK;
+}
+
+extern "C" int vrt_secondary_spill_stats(vrt_scene *s, int64_t stats[6])
+{
+        if (s && need_device(s))
+                return VRT_E_NODEVICE;
+        if (!s || !stats)
+                return fail(VRT_E_INVALID, "null argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        for (int r = 0; r < 6; ++r)
+                stats[r] = 0;
+        if (s->spill_last < 0 || !s->d_spill[s->spill_last])
+                return VRT_OK;
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipEventSynchronize(s->spill_ev[s->spill_last]));
+        uint32_t c[8];
+        HIPCHK(hipMemcpy(c, s->d_spill[s->spill_last], sizeof c, hipMemcpyDeviceToHost));
+        stats[0] = c[2];                     // records queued (spill_close)
+        stats[1] = c[5];                     // rays finished in place, queue full (spill_room)
+        stats[2] = std::min(c[0], s->spill_cap[s->spill_last]);  // chunks taken
+        stats[3] = s->spill_cap[s->spill_last];                  // chunks allocated
+        stats[4] = c[3];                     // chunks left to the batch-pool launch
+        stats[5] = (int64_t)sizeof(SpillRec);
         return VRT_OK;
 }
 
@@ -2210,7 +2243,10 @@ static int trace_scratch(vrt_scene *s, int set, const TraceParams &tp, TracePara
         const size_t need = head + nslots * 64 + 512 + nslots * 4;
         if (t.rec_bytes < need) {
                 if (t.rec) {
-                        HIPCHK(hipDeviceSynchronize());  // callers may have queued work on any stream
+                        // every user of the set's scratch is ordered by its event
+                        // (ts_acquire waits for it, ts_release records it)
+                        if (t.live)
+                                HIPCHK(hipEventSynchronize(t.ev));
                         (void)hipFree(t.rec);
                         t.rec = nullptr;
                         t.rec_bytes = 0;
@@ -2220,10 +2256,9 @@ static int trace_scratch(vrt_scene *s, int set, const TraceParams &tp, TracePara
                 t.steps_key[0] = t.steps_key[1] = -1.f;
         }
         // the step table depends on mindist and maxdist only: rebuilt when
-        // they change (the set's users are ordered by its event)
+        // they change (the set's users are ordered by its event); the key is
+        // committed only once k_cone_steps is enqueued (steps_commit)
         out->build_steps = !(t.steps_key[0] == tp.mindist && t.steps_key[1] == tp.maxdist);
-        t.steps_key[0] = tp.mindist;
-        t.steps_key[1] = tp.maxdist;
         char *b = static_cast<char *>(t.rec);
         out->steps = reinterpret_cast<float4 *>(b);
         out->nsteps = reinterpret_cast<int *>(b + (size_t)kConeSteps * 16);
@@ -2231,6 +2266,17 @@ static int trace_scratch(vrt_scene *s, int set, const TraceParams &tp, TracePara
         out->tail_n = reinterpret_cast<unsigned int *>(b + head + nslots * 64);
         out->tail = reinterpret_cast<uint32_t *>(b + head + nslots * 64 + 512);
         return VRT_OK;
+}
+
+// After launch_trace_prim returned success: the step table it was asked to
+// build (k_cone_steps) is enqueued, so the set's key may say so.  Every error
+// return before that leaves the key as it was, and the next call rebuilds.
+static void steps_commit(vrt_scene *s, int set, const TraceParams &tp)
+{
+        if (!tp.build_steps || tp.r.tiles_this_rank <= 0)
+                return;
+        s->ts[set].steps_key[0] = tp.mindist;
+        s->ts[set].steps_key[1] = tp.maxdist;
 }
 
 // The cone march's split level as a function of the diameter
@@ -2337,6 +2383,7 @@ extern "C" int vrt_render_trace_device(vrt_scene *s, const vrt_camera *cam, cons
                 return rc;
         HIPCHK(hipEventRecord(s->ev0, st));
         HIPCHK(launch_trace(tp, st));
+        steps_commit(s, set, tp);
         HIPCHK(hipEventRecord(s->ev1, st));
         if (int rc = ts_release(s, set, st))
                 return rc;
@@ -2393,6 +2440,7 @@ extern "C" int vrt_trace_frame_device(vrt_scene *s, const vrt_camera *light_cam,
                 if (int rc = ts_acquire(s, set, st))
                         return rc;
                 HIPCHK(launch_trace_prim(tp, st));
+                steps_commit(s, set, tp);
                 return VRT_OK;
         };
         if (int rc = lightmap_enqueue(s, set, light_cam, light_film, &nhit, overlap, s->lm_ev)) {
@@ -2456,6 +2504,7 @@ extern "C" int vrt_render_trace(vrt_scene *s, const vrt_camera *cam, const vrt_f
                 return rc;
         HIPCHK(hipEventRecord(s->ev0, s->stream));
         HIPCHK(launch_trace(tp, s->stream));
+        steps_commit(s, set, tp);
         HIPCHK(hipEventRecord(s->ev1, s->stream));
         if (int rc = ts_release(s, set, s->stream))
                 return rc;

@@ -1897,12 +1897,13 @@ __device__ __forceinline__ uint32_t take_unit(uint32_t *ctr)
 // Persistent variant (uninstrumented, no per-sample outputs): 4-wave
 // workgroups sized to fill the chip once; every wave pulls quadrant units
 // from a per-XCD counter (blocks b, b+8, ... share an XCD and its L2; an
-// XCD's counter covers one contiguous slice of the tiles) and, once its own
-// slice is exhausted, from the other XCDs' counters.
-// One-wave workgroups top out at 16 resident waves per CU (the per-CU
-// workgroup limit); at VRT_PERSIST_WAVES_PER_EU = 5 this kernel keeps 5
-// waves per SIMD = 20 per CU resident, and a wave never waits for a
-// workgroup sibling.  The counters belong to this launch alone (WorkQueue,
+// XCD's counter covers slice x of the units, 512-unit chunks dealt round
+// robin to the 8 slices, slice_unit) and, once its own slice is exhausted,
+// from the next XCD's counter (kPersistHelp).
+// At VRT_PERSIST_WAVES_PER_EU = 6 (80 VGPRs, no scratch) the 256-thread
+// workgroups keep 6 waves per SIMD = 24 per CU resident; the waves of a
+// workgroup share nothing but its LDS stack array, so none waits for a
+// sibling.  The counters belong to this launch alone (WorkQueue,
 // vrt_internal.h): nothing is reset at the end.
 // kFastOnly (camera rays of a finite scene, decided on the host): only the
 // fast standard-range march is compiled in; a wave with a ray that needs the

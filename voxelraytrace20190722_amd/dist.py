@@ -38,12 +38,15 @@ def deal_block():
 def deal_weight(nranks):
     """(m, V) of the weighted deal (vrt_internal.h VRT_DEAL_WEIGHT): from 2
     ranks on, rank 0 -- which also gathers and re-assembles the frame -- gets
-    (m-1)/m of another rank's blocks, m = max(2, 48 // nranks); the whole
+    (m-1)/m of another rank's blocks, m = max(2, SPAN // nranks); the whole
     blocks run in periods of V = m*nranks - 1 turns, position p of a period
-    going to rank nranks-1 - p % nranks.  (0, 0): plain round robin."""
-    if nranks < 2:
+    going to rank nranks-1 - p % nranks.  (0, 0): plain round robin.  The
+    switch and SPAN are the library build's (vrt_build_flag), as deal_block's
+    G is, so a variant build and these helpers deal the same tiles."""
+    from .api import build_flag
+    if nranks < 2 or not build_flag("VRT_DEAL_WEIGHT"):
         return 0, 0
-    m = max(2, 48 // nranks)
+    m = max(2, int(build_flag("VRT_DEAL_SPAN")) // nranks)
     return m, m * nranks - 1
 
 
