@@ -41,9 +41,31 @@ MAX_CLOCK_GHZ = 2.4     # MI355X max engine clock (MI355X_MICROARCH.md chip tabl
 
 
 CPU_NOTE = ("kind 'port': oracle/vrt_oracle.c, the C restatement of the reference path, scheduled as render_mt "
-            "(64 tile tasks over hardware_concurrency threads); the reference's own thread_pool_cpp path cannot "
-            "be built here without stand-ins for headers libstdc++ 11 lacks (SURVEY §8(c), DESIGN §2), so no "
-            "calibration ratio to it exists (BASELINE.md)")
+            "(64 tile tasks over min(hardware_concurrency, 64) threads taking tiles from an atomic counter); the "
+            "reference's own per-pixel code (camera.cc, voxel_octree.cc) cannot be built here without stand-ins "
+            "for headers libstdc++ 11 lacks (SURVEY §8(c), DESIGN §2), but its scheduler can: "
+            "calibration_ratio = this scheduler's frame time / the reference's thread_pool_cpp's (compiled "
+            "unmodified, driving the same oracle render, tools/cpu_calibration.py in the build container; "
+            "the reference never travels to the GPU box), so value x ratio = the reference scheduler's rate")
+CALIB_JSON = os.path.join(ROOT, "tests", "golden", "cpu_calibration.json")
+
+
+def cpu_calibration():
+    """The committed thread_pool_cpp calibration (tools/cpu_calibration.py):
+    {calibration_ratio, ...} or None."""
+    try:
+        c = json.load(open(CALIB_JSON))
+    except (OSError, ValueError):
+        return None
+    b = c.get("box_shaped", {})
+    return {"calibration_ratio": c.get("calibration_ratio"),
+            "calibration": {"source": "tests/golden/cpu_calibration.json (tools/cpu_calibration.py)",
+                            "measured_on": f"{c.get('nproc')} CPUs of the build container ({c.get('cpu_model')})",
+                            "config": c.get("config"),
+                            "box_shaped": {k: b.get(k) for k in ("pool_workers", "oracle_threads", "calibration_ratio")},
+                            "native": {k: c.get("native", {}).get(k) for k in ("pool_workers", "oracle_threads",
+                                                                              "calibration_ratio")},
+                            "ratio_def": c.get("ratio_def")}}
 
 
 def log(*a):
@@ -1168,6 +1190,10 @@ def main():
                          f" {rays_per_frame} rays each, median frame), oracle/vrt_oracle.c with render_mt's 64 "
                          f"tile tasks over {nth} threads (hardware_concurrency = {ci['nproc']}, capped at the 64 "
                          f"tasks); all {checked} frames bit-identical to the GPU image of the same pose"}
+        cal = cpu_calibration()
+        if cal and cal["calibration_ratio"]:
+            cpu.update(cal)
+            cpu["reference_scheduler_value"] = round(cpu["value"] * cal["calibration_ratio"], 4)
         osc.close()
 
     data_desc = (f"OBJ scene {a.scene} (tinyobj-exact ingest)" if a.scene else

@@ -1028,6 +1028,30 @@ double ora_render_rows(const ora_scene *s, const float cam[19], float film_w,
         return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
 }
 
+/* One render_mt task (VRT/camera.h:50-60): pixels [x0, x1) x [y0, y1),
+ * rows py then columns px, film index y*nx+x; rgb accumulated into.  The
+ * caller schedules the tasks (oracle/pool_calib.cc drives it with the
+ * reference's own thread_pool_cpp). */
+void ora_render_tile(const ora_scene *s, const float cam[19], float film_w,
+                     float film_h, int nx, int ny, int x0, int y0, int x1,
+                     int y1, float *rgb)
+{
+        rjob j;
+        memset(&j, 0, sizeof j);
+        j.s = s;
+        j.cam = cam;
+        j.fw = film_w;
+        j.fh = film_h;
+        j.nx = nx;
+        j.ny = ny;
+        j.film_index = 1;
+        j.row_stride = 1;
+        j.rgb = rgb;
+        for (int py = y0; py < y1; ++py)
+                for (int px = x0; px < x1; ++px)
+                        render_pixel(&j, px, py);
+}
+
 /* stbiw__linear_to_rgbe: VRT/stb_image_write.h:601-616 */
 void ora_linear_to_rgbe(const float lin[3], uint8_t rgbe[4])
 {

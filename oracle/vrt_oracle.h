@@ -114,6 +114,12 @@ double ora_render_rows(const ora_scene *s, const float cam[19], float film_w,
                        float film_h, int nx, int ny, int row_stride,
                        int row_phase, int nthreads, float *rgb);
 
+/* One render_mt task (VRT/camera.h:50-60): pixels [x0,x1) x [y0,y1), rows
+ * then columns, film index y*nx+x, accumulated into rgb (nx*ny*3). */
+void ora_render_tile(const ora_scene *s, const float cam[19], float film_w,
+                     float film_h, int nx, int ny, int x0, int y0, int x1,
+                     int y1, float *rgb);
+
 /* jql::PCG (VRT/graphics_math.h:821-857): one operator() call. */
 uint32_t ora_pcg_next(uint64_t *state);
 /* std::uniform_real_distribution<float>{-1, 1}(pcg) as libstdc++ 11 does it

@@ -27,6 +27,7 @@ def main():
     dev = torch.device("cuda:0")
     prim = torch.zeros(a.width * a.height * 8, dtype=torch.float32, device=dev)
     vis = torch.zeros((a.height, a.width), dtype=torch.float32, device=dev)
+    tot = []
     for i in range(a.poses):
         fov, eye, spot, up = vrt.sweep_pose(mn, mx, i, 16)
         cam = vrt.Camera(fov, eye, spot, up)
@@ -36,7 +37,14 @@ def main():
             tree.render_secondary_device(cam, film, 64, 0, 1, prim.data_ptr(), vis.data_ptr(), None)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3
-        print(f"pose {i}: {ms:.2f} ms, spill counts {tree.secondary_spill_counts()}", flush=True)
+        st = tree.secondary_spill_stats()
+        tot.append(st)
+        print(f"pose {i}: {ms:.2f} ms, spill stats {st}", flush=True)
+    n = len(tot)
+    rec = sum(t["records"] for t in tot) / n
+    fin = sum(t["finished_in_place"] for t in tot) / n
+    print(f"mean per frame: {rec:.0f} records ({rec * tot[0]['record_bytes'] / 1e9:.3f} GB of records), "
+          f"{fin:.0f} finished in place", flush=True)
 
 
 if __name__ == "__main__":
