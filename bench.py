@@ -38,6 +38,9 @@ N_CU = 256              # MI355X compute units (4 SIMD-32 each)
 # (MI355X_MICROARCH.md "Wave scheduling"), 4 SIMDs per CU
 VALU_WAVE_INSTR_PER_CYCLE = N_CU * 4 / 2
 MAX_CLOCK_GHZ = 2.4     # MI355X max engine clock (MI355X_MICROARCH.md chip table)
+# SALU issue peak: one scalar unit per CU (MI355X_MICROARCH.md glossary,
+# "CU"), one scalar instruction per cycle
+SALU_INSTR_PER_CYCLE = N_CU * 1
 
 
 CPU_NOTE = ("kind 'port': oracle/vrt_oracle.c, the C restatement of the reference path, scheduled as render_mt "
@@ -276,6 +279,7 @@ def roofline_from_pmc(pmc, kernel, single_ms, out_bytes, ref_bytes, launch_ms=No
         "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "G wave-instr/s",
         "frac": round(achieved / peak, 4),
         "peak_def": f"{N_CU} CUs x 4 SIMDs x 1/2 wave64 VALU instr/cycle x {MAX_CLOCK_GHZ} GHz max clock",
+        "valu_frac": round(achieved / peak, 4),
         "time_basis": {"single_launch_ms": round(single_ms, 4),
                        "note": "one frame in flight: the kernel alone on the GPU (HIP events on its stream)"},
         "issue_frac_at_clock": round(valu / (VALU_WAVE_INSTR_PER_CYCLE * cycles), 4),
@@ -310,6 +314,24 @@ def roofline_from_pmc(pmc, kernel, single_ms, out_bytes, ref_bytes, launch_ms=No
     if launch_ms is not None and launch_ms != single_ms:
         out["time_basis"]["launch_ms"] = round(launch_ms, 4)
         out["time_basis"]["frac_at_launch_ms"] = round(valu / (launch_ms * 1e-3) / 1e9 / peak, 4)
+    if m.get("SQ_INSTS_SALU") is not None:
+        # the scalar pipe: one scalar unit per CU issues for all its waves, so
+        # a kernel heavy in loop / exec-mask control can be bound there before
+        # its VALU issue is; `bound` names the busier of the two pipes and the
+        # top-level achieved / peak / frac are that pipe's
+        salu = m["SQ_INSTS_SALU"]
+        s_ach = salu / t / 1e9
+        s_peak = SALU_INSTR_PER_CYCLE * MAX_CLOCK_GHZ
+        out["salu_frac"] = round(s_ach / s_peak, 4)
+        out["salu"] = {"achieved": round(s_ach, 1), "peak": round(s_peak, 1), "unit": "G instr/s",
+                       "frac": round(s_ach / s_peak, 4), "instr_per_launch": round(salu),
+                       "issue_frac_at_clock": round(salu / (SALU_INSTR_PER_CYCLE * cycles), 4),
+                       "peak_def": f"{N_CU} CUs x 1 scalar unit x 1 SALU instr/cycle x {MAX_CLOCK_GHZ} GHz max clock"}
+        out["valu"] = {"achieved": out["achieved"], "peak": out["peak"], "unit": "G wave-instr/s",
+                       "frac": out["valu_frac"], "peak_def": out["peak_def"]}
+        if out["salu_frac"] > out["valu_frac"]:
+            out.update({"bound": "salu", "achieved": out["salu"]["achieved"], "peak": out["salu"]["peak"],
+                        "unit": "G instr/s", "frac": out["salu_frac"], "peak_def": out["salu"]["peak_def"]})
     if pmc.get("skipped"):
         out["pmc_skipped"] = pmc["skipped"]
     return out

@@ -449,3 +449,24 @@ def test_camera_defer_bound_is_an_upper_bound():
         cam = vrt.Camera(*vrt.sweep_pose(mn, mx, k, 16))
         assert bounds[k] >= _deferring_rays(cam, vrt.Film(1, 1, 320, 180))
     assert max(bounds) < 64
+
+
+def test_roofline_names_the_busier_issue_pipe():
+    """bench.roofline_from_pmc: VALU issue against 256 CUs x 4 SIMDs x 1/2 x
+    2.4 GHz, SALU issue against 256 CUs x 1 x 2.4 GHz; `bound` and the
+    top-level achieved / peak / frac are the busier pipe's."""
+    import bench
+    base = {"FETCH_SIZE": 1000.0, "WRITE_SIZE": 500.0, "GRBM_GUI_ACTIVE": 8 * 2.4e6, "SQ_WAVES": 100.0,
+            "SQ_WAVE_CYCLES": 1e6, "TCC_HIT_sum": 3.0, "TCC_MISS_sum": 1.0}
+    t_ms = 1.0
+    for valu, salu, want in [(600e6, 100e6, "valu"), (400e6, 400e6, "salu")]:
+        pmc = {"per_kernel": {"k": dict(base, SQ_INSTS_VALU=valu, SQ_INSTS_SALU=salu)}, "dispatch": {},
+               "kernel_stats": {}, "child_kernel_ms": t_ms}
+        r = bench.roofline_from_pmc(pmc, "k", t_ms, 1, None)
+        vf = valu / 1e-3 / 1e9 / (256 * 4 / 2 * 2.4)
+        sf = salu / 1e-3 / 1e9 / (256 * 2.4)
+        assert r["valu_frac"] == pytest.approx(vf, abs=1e-4)
+        assert r["salu_frac"] == pytest.approx(sf, abs=1e-4)
+        assert r["bound"] == want
+        assert r["frac"] == pytest.approx(max(vf, sf), abs=1e-4)
+        assert r["salu"]["instr_per_launch"] == round(salu)

@@ -41,9 +41,10 @@ def main():
                                         r.get("reference_equivalent_bytes_per_launch"),
                                         launch_ms=tb.get("launch_ms"), child_ms=child_ms)
     keys = ("achieved", "peak", "frac", "issue_frac_at_clock", "traffic", "l2_hit", "frac_fp64_weighted",
-            "lane_utilisation")
+            "lane_utilisation", "valu_frac", "salu_frac")
     check = {k: (r.get(k), again.get(k)) for k in keys}
     check["hbm_frac"] = (r["hbm"]["frac"], again["hbm"]["frac"])
+    check["bound_is_salu"] = (float(r["bound"] == "salu"), float(again["bound"] == "salu"))
     ok = all(abs((a or 0) - (b or 0)) <= 1e-3 * max(1.0, abs(a or 0)) for a, b in check.values())
     trace_avg = stats.get(kern, (None, None, None))[1]
     summ = {"bench_json": os.path.basename(bj), "build_id": line.get("build_id"), "kernel": meta[kern]["kernel"],
