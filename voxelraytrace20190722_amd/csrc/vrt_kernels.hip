@@ -1569,6 +1569,14 @@ __device__ __forceinline__ void spill_read(const SpillRec *q, uint4 &h, f3 &d, u
         }
 }
 
+// (float)spp at the point of use: the compiler otherwise hoists the
+// conversion out of the persistent loops into a VGPR it spills
+__device__ __forceinline__ float spp_f(int32_t spp)
+{
+        asm volatile("" : "+s"(spp));
+        return (float)spp;
+}
+
 // lane 0 adds n to *ctr, the wave reads lane 0's result (as take_unit)
 __device__ __forceinline__ uint32_t take_n(uint32_t *ctr, uint32_t n)
 {
@@ -2293,7 +2301,7 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         const uint64_t sm = kAny ? __ballot(spilled) : 0ull;
         if (lane == 0) {
                 if (sm == 0)
-                        p.vis[vi] = (float)(p.spp - (int)__popcll(hm)) / (float)p.spp;
+                        p.vis[vi] = (float)(p.spp - (int)__popcll(hm)) / spp_f(p.spp);
                 else  // hits so far << 8 | rays still out: the resume rounds finish the pixel
                         reinterpret_cast<uint32_t *>(p.prim + 8 * pix)[7] =
                                 ((uint32_t)__popcll(hm) << 8) | (uint32_t)__popcll(sm);
@@ -2363,7 +2371,7 @@ __device__ __forceinline__ void resume_pool_chunk(const ResumeParams &p, const S
                         float *pr = p.prim + 8 * (size_t)pix;
                         const uint32_t old = atomicAdd(reinterpret_cast<uint32_t *>(pr) + 7, hit ? 255u : 0xFFFFFFFFu);
                         if ((old & 0xFFu) == 1u)  // the pixel's last ray
-                                p.vis[vi] = (float)(p.spp - (int)((old >> 8) + hit)) / (float)p.spp;
+                                p.vis[vi] = (float)(p.spp - (int)((old >> 8) + hit)) / spp_f(p.spp);
                 }
                 wave_lds_sync();  // dirs / opix / mbox / hword are rewritten by the next batch
         }
@@ -2636,7 +2644,7 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
                                 float *pr = p.prim + 8 * (size_t)pix;
                                 const uint32_t old = atomicAdd(reinterpret_cast<uint32_t *>(pr) + 7, h ? 255u : 0xFFFFFFFFu);
                                 if ((old & 0xFFu) == 1u)  // the pixel's last ray
-                                        p.vis[vi] = (float)(p.spp - (int)((old >> 8) + h)) / (float)p.spp;
+                                        p.vis[vi] = (float)(p.spp - (int)((old >> 8) + h)) / spp_f(p.spp);
                         }
                         assigned &= ~done;
                 }
