@@ -281,6 +281,10 @@ int vrt_device_selftest(int device, const double *mt_in, double *mt_out,
 /* VRT_TEST_PRIM_TAIL does the same for the primary pass of the cone-traced
  * render (vrt_render_trace*, vrt_trace_frame_device). */
 #define VRT_TEST_PRIM_TAIL 64
+/* VRT_TEST_SEC_DEFER: config 5's fast-only walk kernel defers every odd
+ * pixel of its rank to the exact-walk launch after it (k_secondary_defer),
+ * as it does a pixel with a ray off the fast walk. */
+#define VRT_TEST_SEC_DEFER 128
 #define VRT_TEST_VIRTUAL_RANKS_N(n) (VRT_TEST_VIRTUAL_RANKS | ((n) << 8))
 int vrt_set_test_flags(int flags);
 /* The current vrt_set_test_flags value (so a caller can restore it). */
@@ -295,8 +299,10 @@ int vrt_secondary_spill_counts(vrt_scene *s, int64_t counts[4]);
  * stats[0] records queued, [1] stopped rays finished in place because the
  * queue was full, [2] queue chunks taken, [3] chunks allocated, [4] chunks
  * left to the batch-pool launch after the streaming round, [5] bytes per
- * record.  All 0 when that launch used no compaction. */
-int vrt_secondary_spill_stats(vrt_scene *s, int64_t stats[6]);
+ * record, [6] pixels deferred from the fast-only walk kernel to the exact
+ * walk (a ray with a zero or tiny direction component).  All 0 when that
+ * launch used no compaction. */
+int vrt_secondary_spill_stats(vrt_scene *s, int64_t stats[7]);
 /* Device bytes the scene holds beyond its octree, triangles and textures
  * (vrt_scene_info().device_bytes): per-call scratch kept between calls --
  * config 5's compaction queues (*spill_bytes, may be NULL), the light-map

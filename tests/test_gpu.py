@@ -366,7 +366,9 @@ def test_secondary_occlusion_walk_matches_ordered_walk(proxy_small, depth):
 
 @pytest.mark.parametrize("depth", [6, 8])
 @pytest.mark.parametrize("flags,spp", [(0, 64), (vrt.TEST_SPILL_ALL, 64), (0, 17), (0, 1),
-                                       (vrt.TEST_SPILL_ALL | vrt.TEST_STREAM_LEFTOVER, 64)])
+                                       (vrt.TEST_SPILL_ALL | vrt.TEST_STREAM_LEFTOVER, 64),
+                                       (vrt.TEST_SEC_DEFER, 64), (vrt.TEST_SEC_DEFER, 17),
+                                       (vrt.TEST_SEC_DEFER | vrt.TEST_SPILL_ALL, 64)])
 def test_secondary_compaction_matches_oracle(proxy_small, depth, flags, spp):
     """Config-5 ray compaction: rays still walking when few
     lanes of their wave are go to a queue with their walk state and are
@@ -378,7 +380,9 @@ def test_secondary_compaction_matches_oracle(proxy_small, depth, flags, spp):
     slot refilled with the next saved ray as soon as its ray ends
     (resume_stream); TEST_STREAM_LEFTOVER sends every odd
     chunk to the batch pool (occl_pool) launched after it; spp < 64 starts
-    with idle lanes."""
+    with idle lanes; TEST_SEC_DEFER sends every odd pixel from the fast-only
+    walk kernel to the exact-walk launch after it (k_secondary_defer), as a
+    pixel with a ray off the fast walk is."""
     tree = vrt.VoxelOctree(proxy_small, depth)
     osc = po.Scene(proxy_small, depth)
     mn, mx = tree.root_box
@@ -388,9 +392,14 @@ def test_secondary_compaction_matches_oracle(proxy_small, depth, flags, spp):
     try:
         vis, rays, d = tree.render_secondary(vrt.Camera(fov, eye, spot, up), film, spp=spp, ids="hit")
         counts = tree.secondary_spill_counts()
+        stats = tree.secondary_spill_stats()
     finally:
         vrt.set_test_flags(0)
     ovis, orays, od = osc.render_secondary(po.camera(fov, eye, spot, up), 1.0, 1.0, 96, 64, spp=spp)
+    if flags & vrt.TEST_SEC_DEFER:  # every odd pixel with a primary hit went to the exact-walk launch
+        assert stats["deferred_pixels"] > 96 * 64 // 8, stats
+    else:  # the fast-only kernel ran: no pixel of this view has a ray off the fast walk
+        assert stats["deferred_pixels"] <= 4, stats
     assert rays == orays
     assert np.array_equal(d["hit"], od["hit"])
     assert np.array_equal(bits(vis), bits(ovis))

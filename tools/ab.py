@@ -83,7 +83,7 @@ def main():
         libs[0].vrt_camera_init(fov, eye.ctypes.data_as(_ffi.f32p), spot.ctypes.data_as(_ffi.f32p),
                                 up.ctypes.data_as(_ffi.f32p), 0.0, vrt.FLT_MAX, C.byref(cam))
         cams.append(cam)
-    if a.share_ranks > 1:
+    if a.share_ranks >= 1:  # 1: the whole frame, frames in flight (the bench's schedule)
         return share_ab(a, libs, scenes, film, cams)
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream(dev)

@@ -10,7 +10,7 @@ from .api import (  # noqa: F401
     FLT_MAX, Camera, Film, MultiOctree, ObjModel, SceneData, VoxelOctree, multi_tile_map, build_id, build_flag, test_flags, device_count, device_selftest,
     device_selftest_order,
     hdr_bytes, hdr_bytes_from_rgbe, intersect_triangle3, load_image, make_ray, obj2voxel, ray_march, ray_march_init,
-    TEST_FORCE_DEFER, TEST_FAIL_LAUNCH, TEST_SPILL_ALL, TEST_STREAM_LEFTOVER, TEST_LIGHT_TAIL, TEST_PRIM_TAIL, TEST_VIRTUAL_RANKS, render, set_test_flags, sweep_pose, tga_decode, tile_deal_map, tiles_per_rank, to_radian, tri_box_overlap,
+    TEST_FORCE_DEFER, TEST_FAIL_LAUNCH, TEST_SPILL_ALL, TEST_STREAM_LEFTOVER, TEST_LIGHT_TAIL, TEST_PRIM_TAIL, TEST_SEC_DEFER, TEST_VIRTUAL_RANKS, render, set_test_flags, sweep_pose, tga_decode, tile_deal_map, tiles_per_rank, to_radian, tri_box_overlap,
     unpack_tiles_device, write_hdr, rgbe_device, write_hdr_device,
 )
 

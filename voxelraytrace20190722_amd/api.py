@@ -433,11 +433,11 @@ class VoxelOctree:
     def secondary_spill_stats(self):
         """The last config-5 launch's compaction (vrt_secondary_spill_stats):
         {records, finished_in_place, chunks_taken, chunks_allocated,
-        leftover_chunks, record_bytes}."""
-        c = (C.c_int64 * 6)()
+        leftover_chunks, record_bytes, deferred_pixels}."""
+        c = (C.c_int64 * 7)()
         check(lib().vrt_secondary_spill_stats(self.h, c), "vrt_secondary_spill_stats")
         return dict(zip(("records", "finished_in_place", "chunks_taken", "chunks_allocated", "leftover_chunks",
-                         "record_bytes"), list(c)))
+                         "record_bytes", "deferred_pixels"), list(c)))
 
     def scratch_bytes(self):
         """(total, compaction) device bytes of scratch the scene keeps between
@@ -739,6 +739,7 @@ TEST_VIRTUAL_RANKS = 8  # include/vrt.h VRT_TEST_VIRTUAL_RANKS (count << 8)
 TEST_STREAM_LEFTOVER = 16  # include/vrt.h VRT_TEST_STREAM_LEFTOVER
 TEST_LIGHT_TAIL = 32  # include/vrt.h VRT_TEST_LIGHT_TAIL
 TEST_PRIM_TAIL = 64  # include/vrt.h VRT_TEST_PRIM_TAIL
+TEST_SEC_DEFER = 128  # include/vrt.h VRT_TEST_SEC_DEFER
 
 
 def set_test_flags(flags):

@@ -372,6 +372,7 @@ struct vrt_scene {
         // the event of its last launch
         void *d_spill[2] = {};
         uint32_t spill_cap[2] = {};  // chunks per queue
+        int64_t spill_px[2] = {};    // deferred-pixel list capacity (pixels)
         hipEvent_t spill_ev[2] = {};
         bool spill_live[2] = {};
         hipStream_t spill_stream[2] = {};  // the set's last user (a stream keeps its set)
@@ -1332,9 +1333,22 @@ static int ts_release(vrt_scene *s, int i, hipStream_t st);
 // compaction) when the build disables it, the film has 2^26 pixels or more,
 // the octree 2^24 nodes or more (SpillRec's packed words), or the allocation
 // fails.
-// chunks: the records, their two fill words and the counters within 1 GiB
-constexpr uint32_t kSpillCapMax =
-        (uint32_t)((((size_t)1 << 30) - 4096) / ((size_t)kSpillChunk * sizeof(SpillRec) + 8));
+// chunks: the records, their two fill words, the counters and the deferred-
+// pixel list (dpb bytes) within 1 GiB
+static uint32_t spill_cap_max(size_t dpb)
+{
+        return (uint32_t)((((size_t)1 << 30) - 4096 - dpb) / ((size_t)kSpillChunk * sizeof(SpillRec) + 8));
+}
+static size_t spill_dpix_bytes(int64_t pixels)
+{
+        return ((size_t)pixels * 4 + 255) & ~(size_t)255;
+}
+static size_t spill_set_bytes(uint32_t nch, int64_t pixels)
+{
+        const size_t fb = ((size_t)nch * 4 + 255) & ~(size_t)255;
+        return (size_t)kSpillMaxRounds * kSpillCtrStride * 4 + 2 * fb + (size_t)nch * kSpillChunk * sizeof(SpillRec) +
+               spill_dpix_bytes(pixels);
+}
 static int spill_setup(vrt_scene *s, int64_t rays, int64_t pixels, hipStream_t st, SpillQueues *sq, int *set)
 {
         *sq = spill_defaults();
@@ -1363,13 +1377,16 @@ static int spill_setup(vrt_scene *s, int64_t rays, int64_t pixels, hipStream_t s
                                      hipHostMallocDefault));
                 std::memset(s->h_spill, 0, 16 * sizeof(uint32_t));
         }
+        // the deferred-pixel list holds one entry per pixel of the film
+        const int64_t px = std::max<int64_t>(pixels, s->spill_px[k]);
+        const uint32_t cap_max = spill_cap_max(spill_dpix_bytes(px));
         // what the finished launches of either set stopped: records queued
         // (ctr[2]) + records finished in place for want of room (ctr[5])
         for (int i = 0; i < 2; ++i)
                 if (s->spill_live[i] && s->spill_cap[i] && hipEventQuery(s->spill_ev[i]) == hipSuccess) {
                         const uint64_t need = (uint64_t)s->h_spill[8 * i + 2] + s->h_spill[8 * i + 5];
                         const uint64_t w = (need * 5 / 4 + kSpillChunk - 1) / kSpillChunk;
-                        s->spill_want = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(s->spill_want, w), kSpillCapMax);
+                        s->spill_want = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(s->spill_want, w), cap_max);
                 }
         if (s->spill_live[k] && s->spill_stream[k] != st)
                 HIPCHK(hipStreamWaitEvent(st, s->spill_ev[k], 0));
@@ -1377,9 +1394,11 @@ static int spill_setup(vrt_scene *s, int64_t rays, int64_t pixels, hipStream_t s
         const int64_t partial = (int64_t)std::max(1, s->dev.sec_blocks) * 4;
         const int64_t est = s->spill_want ? (int64_t)s->spill_want : (rays / 32 + kSpillChunk - 1) / kSpillChunk;
         const uint32_t nch = (uint32_t)std::min<int64_t>(std::min<int64_t>(est, (rays + kSpillChunk - 1) / kSpillChunk) +
-                                                                 partial, kSpillCapMax);
+                                                                 partial, cap_max);
         const size_t ctr_bytes = (size_t)kSpillMaxRounds * kSpillCtrStride * 4;
-        if (s->spill_cap[k] < nch) {
+        if (s->spill_cap[k] < nch || s->spill_px[k] < pixels) {
+                // a regrowth for a larger film keeps the chunks it had
+                const uint32_t c = std::min(std::max(nch, s->spill_cap[k]), cap_max);
                 if (s->d_spill[k]) {
                         // the set's users on any stream are ordered by its event
                         // (spill_done after each, a stream wait when a set
@@ -1389,15 +1408,15 @@ static int spill_setup(vrt_scene *s, int64_t rays, int64_t pixels, hipStream_t s
                         (void)hipFree(s->d_spill[k]);
                         s->d_spill[k] = nullptr;
                         s->spill_cap[k] = 0;
+                        s->spill_px[k] = 0;
                 }
-                const size_t fb = ((size_t)nch * 4 + 255) & ~(size_t)255;
-                if (hipMalloc(&s->d_spill[k], ctr_bytes + 2 * fb + (size_t)nch * kSpillChunk * sizeof(SpillRec)) !=
-                    hipSuccess) {
+                if (hipMalloc(&s->d_spill[k], spill_set_bytes(c, px)) != hipSuccess) {
                         (void)hipGetLastError();
                         s->d_spill[k] = nullptr;
                         return VRT_OK;  // no compaction
                 }
-                s->spill_cap[k] = nch;
+                s->spill_cap[k] = c;
+                s->spill_px[k] = px;
         }
         const size_t fb = ((size_t)s->spill_cap[k] * 4 + 255) & ~(size_t)255;
         char *b = static_cast<char *>(s->d_spill[k]);
@@ -1407,6 +1426,8 @@ static int spill_setup(vrt_scene *s, int64_t rays, int64_t pixels, hipStream_t s
         sq->rec[0] = reinterpret_cast<SpillRec *>(b + ctr_bytes + 2 * fb);
         sq->rec[1] = nullptr;  // the pooled resume round stops no ray
         sq->nchunks = s->spill_cap[k];
+        sq->dpix = reinterpret_cast<uint32_t *>(b + ctr_bytes + 2 * fb +
+                                                (size_t)s->spill_cap[k] * kSpillChunk * sizeof(SpillRec));
         HIPCHK(hipMemsetAsync(sq->ctr, 0, ctr_bytes, st));
         *set = k;
         return VRT_OK;
@@ -1875,11 +1896,8 @@ extern "C" int vrt_scene_scratch_bytes(vrt_scene *s, int64_t *bytes, int64_t *sp
         std::lock_guard<std::mutex> lk(s->mu);
         int64_t sp = 0;
         for (int k = 0; k < 2; ++k)
-                if (s->d_spill[k]) {
-                        const int64_t fb = ((int64_t)s->spill_cap[k] * 4 + 255) & ~(int64_t)255;
-                        sp += (int64_t)kSpillMaxRounds * kSpillCtrStride * 4 + 2 * fb +
-                              (int64_t)s->spill_cap[k] * kSpillChunk * (int64_t)sizeof(SpillRec);
-                }
+                if (s->d_spill[k])
+                        sp += (int64_t)spill_set_bytes(s->spill_cap[k], s->spill_px[k]);
         int64_t t = sp + (int64_t)s->light_bytes + (int64_t)s->ho.bytes;
         for (const TraceSet &ts : s->ts) {
                 if (ts.lm)
@@ -1912,14 +1930,14 @@ extern "C" int vrt_secondary_spill_counts(vrt_scene *s, int64_t counts[4])
         return VRT_OK;
 }
 
-extern "C" int vrt_secondary_spill_stats(vrt_scene *s, int64_t stats[6])
+extern "C" int vrt_secondary_spill_stats(vrt_scene *s, int64_t stats[7])
 {
         if (s && need_device(s))
                 return VRT_E_NODEVICE;
         if (!s || !stats)
                 return fail(VRT_E_INVALID, "null argument");
         std::lock_guard<std::mutex> lk(s->mu);
-        for (int r = 0; r < 6; ++r)
+        for (int r = 0; r < 7; ++r)
                 stats[r] = 0;
         if (s->spill_last < 0 || !s->d_spill[s->spill_last])
                 return VRT_OK;
@@ -1933,6 +1951,7 @@ extern "C" int vrt_secondary_spill_stats(vrt_scene *s, int64_t stats[6])
         stats[3] = s->spill_cap[s->spill_last];                  // chunks allocated
         stats[4] = c[3];                     // chunks left to the batch-pool launch
         stats[5] = (int64_t)sizeof(SpillRec);
+        stats[6] = c[6];                     // pixels deferred to k_secondary_defer (exact walk)
         return VRT_OK;
 }
 

@@ -231,8 +231,11 @@ constexpr int kSpillMaxRounds = 4;
 struct SpillQueues {
         uint32_t *ctr;       // zeroed per frame: [0] chunks taken by phase A, [1] chunks taken by the
                              // stream, [2] records written, [3] chunks the stream left to k_sec_resume,
-                             // [4] their pieces taken, [5] stopped rays finished in place (queue full);
+                             // [4] their pieces taken, [5] stopped rays finished in place (queue full),
+                             // [6] pixels deferred to k_secondary_defer, [7] of them taken;
                              // the words of rounds 1..3 ([r * kSpillCtrStride + 2]) stay 0
+        uint32_t *dpix;      // the deferred pixels (this rank's pixel indices), one per pixel of the
+                             // film at most; NULL: no fast-only kernel
         uint32_t *fill[2];   // [0] records in each chunk of queue 0, written by the chunk's writer;
                              // [1] the chunks the stream left
         SpillRec *rec[2];    // queue 0's records: rec[0] + chunk * kSpillChunk ([1] unused)

@@ -1344,11 +1344,14 @@ __device__ __forceinline__ bool ray_occluded_dispatch(const DevScene &sc, const 
 // fast / exact choice is made per wave as in ray_occluded_dispatch; both
 // walks keep the same state (node indices, child masks of the same hit
 // children), so a state saved by one continues in the other.
-template <int kS, bool kR64>
+template <int kS, bool kR64, bool kFastOnly = false>
 __device__ __forceinline__ int occl_dispatch_spill(const DevScene &sc, const RayK &r, uint2 *stk, OcclState &w,
                                                    bool resume, uint32_t spill_t)
 {
-        if (__all(sc.fast_ok && fast_ok(r) && fin_ok(r))) {
+        // kFastOnly: the caller has checked that every ray of the wave takes the
+        // fast walk (secondary_pixel defers the other pixels): the exact walk is
+        // not compiled in
+        if (kFastOnly || __all(sc.fast_ok && fast_ok(r) && fin_ok(r))) {
                 if (!resume) {
                         const int st = occl_start<true, kR64, true>(sc, r, w);
                         if (st != kOcclWalk)
@@ -2185,6 +2188,7 @@ struct SecondaryParams {
         int32_t *s_hit, *s_tri;
         uint32_t *s_vox;
         int32_t units;         // this rank's pixels (persistent launch)
+        int32_t test_flags;    // VRT_TEST_SEC_DEFER
         WorkQueue q;           // persistent launch only
         SpillQueues sq;        // ray compaction (kAny, persistent launch); sq.nchunks == 0: off
 };
@@ -2200,7 +2204,7 @@ constexpr int kSecPBlock = 256;
 // pts = this wave's 64 sphere points in LDS.
 // kAny (no per-ray ids requested): the visibility image needs only each
 // ray's hit boolean -> the occlusion walk (ray_occluded), same booleans.
-template <bool kR64, bool kAny, int kS>
+template <bool kR64, bool kAny, int kS, bool kFastOnly = false>
 __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_t k, int lane, uint2 *stk,
                                                 float (*pts)[3], SpillCursor &cur)
 {
@@ -2260,42 +2264,58 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         bool hit = false, spilled = false;
         OcclState w;
         f3 dn;
+        RayK r;
         if (lane < p.spp) {
                 const f3 pt = mk3(pts[lane][0], pts[lane][1], pts[lane][2]);
                 dn = normalize(nrm + pt);  // Ray{hit, n + p, res} normalises d
-                const RayK r = make_rayk(hp, dn, p.res, kFltMax);
-                const size_t si = vi * (size_t)p.spp + lane;
-                if (kAny) {
-                        const int res = occl_dispatch_spill<kS, kR64>(p.sc, r, stk, w, false, t);
-                        hit = res == kOcclHit;
-                        spilled = res == kOcclSpill;
-                        if (p.s_hit && !spilled) p.s_hit[si] = hit ? 1 : 0;
-                } else {
-                        MarchResult m;
-                        ray_march_dispatch<false, kS, false, kR64>(p.sc, r, stk, nullptr, nullptr, m);
-                        hit = m.hit;
-                        if (p.s_hit) p.s_hit[si] = m.hit ? 1 : 0;
-                        if (p.s_tri) p.s_tri[si] = m.hit ? (int32_t)m.tri : -1;
-                        if (p.s_vox) p.s_vox[si] = m.hit ? p.sc.node_vox[m.node] : 0xFFFFFFFFu;
-                }
+                r = make_rayk(hp, dn, p.res, kFltMax);
         }
-        if (kAny && t) {
-                const uint64_t sm0 = __ballot(spilled);
-                if (sm0 != 0ull) {
+        if (kFastOnly && (!__all(lane >= p.spp || (fast_ok(r) && fin_ok(r))) ||
+                          ((p.test_flags & VRT_TEST_SEC_DEFER) && (k & 1)))) {
+                // a ray off the fast walk (a zero or tiny direction component):
+                // the pixel goes to the deferred list, which k_secondary_defer
+                // renders with the exact walk after this launch (every lane in
+                // the add, as take_unit; the branch is wave-uniform)
+                const uint32_t j = take_n(p.sq.ctr + 6, 1u);
+                if (lane == 0)
+                        p.sq.dpix[j] = (uint32_t)k;
+                return;
+        }
+        if (kAny) {
+                // one call site for the walk: a group whose stopped rays find
+                // the queue full walks them on in place from where they stopped
+                // (state and LDS stack intact) in a second turn of the loop
+                bool resume = false;
+                uint32_t tt = t;
+                for (;;) {
+                        if (lane < p.spp && (!resume || spilled)) {
+                                const int res = occl_dispatch_spill<kS, kR64, kFastOnly>(p.sc, r, stk, w, resume, tt);
+                                hit = res == kOcclHit;
+                                spilled = res == kOcclSpill;
+                        }
+                        if (!tt)
+                                break;
+                        const uint64_t sm0 = __ballot(spilled);
+                        if (sm0 == 0ull)
+                                break;
                         if (spill_room(p.sq, p.sq.ctr, p.sq.fill[0], cur, (uint32_t)__popcll(sm0))) {
                                 spill_group<kS>(p.sq.rec[0], cur, spilled, (uint32_t)pix, (uint32_t)lane, dn, w,
                                                 stk);
-                        } else if (spilled) {
-                                // the queue is full: the ray walks on in place from where
-                                // it stopped (its state and LDS stack are intact), to its end
-                                const RayK r = make_rayk(mk3(pr[1], pr[2], pr[3]), dn, p.res, kFltMax);
-                                const int res = occl_dispatch_spill<kS, kR64>(p.sc, r, stk, w, true, 0u);
-                                hit = res == kOcclHit;
-                                spilled = false;
-                                if (p.s_hit)
-                                        p.s_hit[vi * (size_t)p.spp + lane] = hit ? 1 : 0;
+                                break;
                         }
+                        resume = true;
+                        tt = 0;
                 }
+                if (p.s_hit && lane < p.spp && !spilled)
+                        p.s_hit[vi * (size_t)p.spp + lane] = hit ? 1 : 0;
+        } else if (lane < p.spp) {
+                const size_t si = vi * (size_t)p.spp + lane;
+                MarchResult m;
+                ray_march_dispatch<false, kS, false, kR64>(p.sc, r, stk, nullptr, nullptr, m);
+                hit = m.hit;
+                if (p.s_hit) p.s_hit[si] = m.hit ? 1 : 0;
+                if (p.s_tri) p.s_tri[si] = m.hit ? (int32_t)m.tri : -1;
+                if (p.s_vox) p.s_vox[si] = m.hit ? p.sc.node_vox[m.node] : 0xFFFFFFFFu;
         }
         const uint64_t hm = __ballot(hit);
         const uint64_t sm = kAny ? __ballot(spilled) : 0ull;
@@ -2707,7 +2727,7 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_sec_resum
 // WorkQueue (XCD x owns a contiguous slice of this rank's pixels, then
 // helps the others), so no wave waits for a slow pixel of a sibling and the
 // resident-wave count is not capped by the per-CU workgroup limit.
-template <bool kR64, bool kAny>
+template <bool kR64, bool kAny, bool kFastOnly>
 __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary_p(SecondaryParams p)
 {
         __shared__ uint2 stk[kStack * kSecPBlock];
@@ -2726,13 +2746,40 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
                         const uint32_t u = take_unit(p.q.ctr + x * kQueueStride) - p.q.base[x];
                         if (u >= (uint32_t)n)
                                 break;
-                        secondary_pixel<kR64, kAny, kSecPBlock>(
+                        secondary_pixel<kR64, kAny, kSecPBlock, kFastOnly>(
                                 p, (int64_t)slice_unit(p.units, x, (int)u, VRT_SEC_SLICE_CHUNK), lane, stk + tid,
                                 pts[wave], cur);
                 }
         }
         if (kAny)
                 spill_close(p.sq.fill[0], p.sq.ctr, cur);
+}
+
+// The pixels k_secondary_p<.., kFastOnly> deferred (a ray off the fast walk;
+// normally a few per frame, none in most): each on the general walk, without
+// compaction (the pixel writes its visibility directly).  No deferred pixel:
+// every wave returns after one scalar load.  Launched after the fast kernel
+// (and the resume rounds) on the same stream, so the list is complete.
+template <bool kR64>
+__global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary_defer(SecondaryParams p)
+{
+        __shared__ uint2 stk[kStack * kSecPBlock];
+        __shared__ float pts[kSecPBlock / 64][64][3];
+        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        const uint32_t n = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(p.sq.ctr + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (n == 0)
+                return;
+        SpillCursor cur;
+        cur.chunk = kSpillFull;  // no compaction here
+        cur.fill = 0;
+        for (;;) {
+                const uint32_t j = take_n(p.sq.ctr + 7, 1u);
+                if (j >= n)
+                        break;
+                const uint32_t k = __builtin_amdgcn_readfirstlane(p.sq.dpix[j]);
+                secondary_pixel<kR64, true, kSecPBlock, false>(p, (int64_t)k, lane, stk + tid, pts[wave], cur);
+        }
 }
 
 #ifndef VRT_SEC_SPILL_T
@@ -2783,6 +2830,7 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
         sp.s_hit = s_hit;
         sp.s_tri = s_tri;
         sp.s_vox = s_vox;
+        sp.test_flags = rp.test_flags;
         // pixels of this rank: its 8x8 tiles (tile_deal)
         const int64_t mine = deal_count(tile_deal(rp.ntx, rp.nty, nranks), rank);
         const int64_t waves = mine * 64;
@@ -2798,9 +2846,15 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                 sp.q = *q;
                 const int cap = nranks > 1 ? std::max(8, rp.sc.sec_blocks - kCollectiveReserve) : rp.sc.sec_blocks;
                 const int g = (int)std::min<int64_t>(cap, ((waves + 3) / 4 + 7) & ~7LL);
-                void (*kern)(SecondaryParams) = w ? (any ? k_secondary_p<true, true> : k_secondary_p<true, false>)
-                                                  : (any ? k_secondary_p<false, true> : k_secondary_p<false, false>);
                 const bool spill = any && sq && sq->t_first > 0 && sq->nchunks > 0;
+                // with compaction (and its deferred-pixel list) in a scene the
+                // fast walk covers, the fast-only kernel: the exact walk's waves
+                // go to k_secondary_defer
+                const bool fo = spill && sq->dpix && sp.sc.fast_ok;
+                void (*kern)(SecondaryParams) =
+                        fo ? (w ? k_secondary_p<true, true, true> : k_secondary_p<false, true, true>)
+                           : w ? (any ? k_secondary_p<true, true, false> : k_secondary_p<true, false, false>)
+                               : (any ? k_secondary_p<false, true, false> : k_secondary_p<false, false, false>);
                 if (spill) {
                         sp.sq = *sq;
                         if (rp.test_flags & VRT_TEST_SPILL_ALL)  // test hook: stop at the first ray's end
@@ -2836,6 +2890,14 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                         // the chunks the stream left (normally none): a small batch-pool launch
                         hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(8), dim3(kSecPBlock), 0,
                                            st, rp2);
+                }
+                if (fo) {
+                        // the deferred pixels (normally a few): a quarter of the
+                        // resident grid, each wave gone after one load if none
+                        SecondaryParams dp = sp;
+                        dp.sq.t_first = 0;
+                        hipLaunchKernelGGL(w ? k_secondary_defer<true> : k_secondary_defer<false>,
+                                           dim3((unsigned)std::max(8, (g / 4) & ~7)), dim3(kSecPBlock), 0, st, dp);
                 }
                 return hipGetLastError();
         }
@@ -3129,11 +3191,13 @@ hipError_t persistent_blocks(int *render_blocks, int *sec_blocks)
                 return e;
         *render_blocks = std::min(a, b);
         int sb = 1 << 30;
-        const void *sk[4] = { reinterpret_cast<const void *>(k_secondary_p<false, false>),
-                              reinterpret_cast<const void *>(k_secondary_p<false, true>),
-                              reinterpret_cast<const void *>(k_secondary_p<true, false>),
-                              reinterpret_cast<const void *>(k_secondary_p<true, true>) };
-        for (int i = 0; i < 4 && e == hipSuccess; ++i)
+        const void *sk[6] = { reinterpret_cast<const void *>(k_secondary_p<false, false, false>),
+                              reinterpret_cast<const void *>(k_secondary_p<false, true, false>),
+                              reinterpret_cast<const void *>(k_secondary_p<true, false, false>),
+                              reinterpret_cast<const void *>(k_secondary_p<true, true, false>),
+                              reinterpret_cast<const void *>(k_secondary_p<false, true, true>),
+                              reinterpret_cast<const void *>(k_secondary_p<true, true, true>) };
+        for (int i = 0; i < 6 && e == hipSuccess; ++i)
                 sb = std::min(sb, resident_blocks(sk[i], kSecPBlock, prop, &e));
         *sec_blocks = sb;
         return e;
