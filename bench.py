@@ -623,7 +623,7 @@ def main():
     local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    rehearse = world == 1 and a.rehearse_ranks > 1 and a.mode == "primary"
+    rehearse = world == 1 and a.rehearse_ranks > 1 and a.mode in ("primary", "secondary")
     if world > 1:
         if a.dist_backend == "nccl":
             # the collectives' stream at high priority: their kernels are
@@ -706,6 +706,13 @@ def main():
             _, frame_rays[pi] = tree.render_secondary(cams[pi], film, spp=a.spp)
         prims = [torch.zeros(W8 * H8 * 8, dtype=torch.float32, device=dev) for _ in range(nbuf)]
         visb = [torch.zeros((a.height, a.width), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+        if nshare > 1:
+            # each rank packs its tiles' pixels (1 float each) and one gather
+            # brings them to rank 0, as the primary frame
+            tiles = [torch.zeros(tpr * 64, dtype=torch.float32, device=dev) for _ in range(nbuf)]
+            gathered = ([torch.zeros((nshare, tpr * 64), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+                        if rank == 0 else None)
+            gl = [list(g[:world].unbind(0)) for g in gathered] if rank == 0 else [None] * nbuf
     elif nshare > 1:
         # the RCCL gather of frame k (on the NCCL stream) overlaps the render
         # of frame k+1
@@ -756,8 +763,8 @@ def main():
             if k is not None:
                 ev_unp[k][0].record(s)
             if secondary:
-                with torch.cuda.stream(s):
-                    imgs[b % nfl].copy_(visb[b])
+                vrt.unpack_tiles_c_device(film, nshare, 1, gathered[b].data_ptr(), imgs[b % nfl].data_ptr(),
+                                          s.cuda_stream)
             else:
                 vrt.unpack_tiles_device(film, nshare, gathered[b].data_ptr(), imgs[b % nfl].data_ptr(),
                                         s.cuda_stream)
@@ -771,32 +778,32 @@ def main():
         s = streams[j]
         if timed:
             ev[k][0].record(s)
-        if world == 1:
+        if nshare == 1:
             tree.render_secondary_device(cam, film, a.spp, 0, 1, prims[j].data_ptr(), imgs[j].data_ptr(),
                                          s.cuda_stream)
             if timed:
                 ev[k][1].record(s)
             return
         finish(b, s)  # frame k - nbuf used these buffers (finished already, same stream)
-        if rank == 0:
-            with torch.cuda.stream(s):
-                visb[b].zero_()  # the previous reduce summed into rank 0's buffer
-        # each rank writes only its own pixels (its tiles of the deal); the
-        # others stay +0.0, so a SUM reduce assembles the image exactly
-        tree.render_secondary_device(cam, film, a.spp, rank, world, prims[b].data_ptr(), visb[b].data_ptr(),
-                                     s.cuda_stream)
+        # this rank's pixels (its tiles of the deal), packed by tile
+        tree.render_secondary_device(cam, film, a.spp, cur["share"], nshare, prims[b].data_ptr(),
+                                     visb[b].data_ptr(), s.cuda_stream)
+        vrt.pack_tiles_c_device(film, cur["share"], nshare, 1, visb[b].data_ptr(), tiles[b].data_ptr(),
+                                s.cuda_stream)
         if timed:
             ev[k][1].record(s)
         if a.dist_backend == "nccl":
             with torch.cuda.stream(s):
-                works[b] = dist.reduce(visb[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
+                works[b] = dist.gather(tiles[b], gl[b], dst=0, async_op=True)
             frame_of[b] = k if (timed and k % DIAG_EVERY == 0) else None
-            finish(sl(k - nfl)[1], s)  # this stream's previous frame: its reduce overlapped this render
-        else:
-            host = visb[b].cpu()
-            dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
+            finish(sl(k - nfl)[1], s)  # this stream's previous frame: its gather overlapped this render
+        else:  # gloo (several ranks on one GPU): host-staged gather
+            host = tiles[b].cpu()
+            hl = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+            dist.gather(host, hl, dst=0)
             if rank == 0:
-                img.copy_(host)
+                gathered[b].copy_(torch.stack(hl))
+                vrt.unpack_tiles_c_device(film, world, 1, gathered[b].data_ptr(), img.data_ptr(), sp)
 
     def render(cam, rk, nr, layout, ptr_, s):
         if trace:
@@ -1123,7 +1130,7 @@ def main():
                          f"({t2_ - t1_:.1f} s, scaled x{(a.width * a.height) / (hw * hh):.0f} to "
                          f"{a.width}x{a.height}) by oracle/vrt_oracle.c over {nth} threads"}
         osc.close()
-    if rank == 0 and world == 1 and not a.no_cpu and secondary:
+    if rank == 0 and world == 1 and not rehearse and not a.no_cpu and secondary:
         # config 5 on the oracle: render_secondary (primary hit + spp rays
         # per pixel, VRT/voxel_octree.cc:600-603 pattern) over min(nproc, 64)
         # threads, 1 warm-up + >= cpu_frames whole frames of the sweep; value
@@ -1263,7 +1270,7 @@ def main():
                       f"(1 primary + {a.spp} stochastic secondary rays per hit pixel)")
             workload = (f"config 5: {a.width}x{a.height} primary hit + {a.spp} spp secondary rays, "
                         f"{scene_name} ({sd.ntri} tris), max_depth {a.depth}")
-            par = f"pixel tiles x{world}" + (f" + {coll} sum-reduce" if world > 1 else "")
+            par = f"pixel tiles x{world}" + (f" + {coll} gather" if world > 1 else "")
         else:
             total_rays = rays_per_frame * a.steps
             mean_rays = rays_per_frame

@@ -205,6 +205,16 @@ int vrt_render_tiles_device(vrt_scene *s, const vrt_camera *cam,
 int vrt_unpack_tiles_device(const vrt_film *film, int nranks,
                             const float *d_gathered, float *d_image,
                             void *stream);
+/* The same deal for images of `comps` floats per pixel (config 5's
+ * visibility image: comps = 1).  Pack: rank `rank`'s tiles of d_image
+ * (ny, nx, comps) -> d_packed, tile k at k * 64 * comps, pixels row-major in
+ * the tile (tiles_per_rank * 64 * comps floats hold any rank's share).
+ * Unpack (rank 0 after the gather): d_gathered = nranks * tiles_per_rank *
+ * 64 * comps floats, rank-major -> d_image (zero outside the tile grid). */
+int vrt_pack_tiles_c_device(const vrt_film *film, int rank, int nranks, int comps, const float *d_image,
+                            float *d_packed, void *stream);
+int vrt_unpack_tiles_c_device(const vrt_film *film, int nranks, int comps, const float *d_gathered, float *d_image,
+                              void *stream);
 /* Device time of the last render kernel enqueued by this thread on `s`
  * (HIP events around the launch, on its stream). */
 int vrt_last_kernel_ms(vrt_scene *s, float *ms);

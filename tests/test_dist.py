@@ -1,7 +1,7 @@
 """Multi-rank frame protocol on CPU (gloo, world_size 2 and 3): the tile
 partition, packed per-rank buffers, gather to rank 0 and re-assembly of
-bench.py's primary frames, and the chunked pixel partition + SUM reduce of
-its secondary frames (voxelraytrace20190722_amd/dist.py).  Ranks render with
+bench.py's primary frames, and the same deal, packing (1 float per pixel),
+gather and re-assembly of its secondary frames (voxelraytrace20190722_amd/dist.py).  Ranks render with
 the oracle (no GPU here); tests/test_gpu.py checks that the device tile
 buffers are exactly dist.pack_tiles_host of the device image."""
 import json
@@ -54,13 +54,18 @@ def _worker(rank, world, port, outdir):
         ref[8 * (ny // 8):] = 0
         ref[:, 8 * (nx // 8):] = 0
         res["primary"] = bool(np.array_equal(full.view(np.uint32), ref.view(np.uint32)))
-    # secondary (config 5): own pixels of a zeroed image, SUM reduce
+    # secondary (config 5): this rank's pixels, packed by tile (1 float per
+    # pixel) -> gather -> unpack on rank 0, as the primary frame; only this
+    # rank's pixels of its image are rendered (the rest is garbage here)
     vis, _ = osc.render_secondary(cam, 1.0, 1.0, nx, ny, spp=4, nthreads=2, ids=False)
-    mine = np.where(vd.secondary_mask(nx, ny, rank, world), vis, np.float32(0))
-    t = torch.from_numpy(np.ascontiguousarray(mine))
-    dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+    mine = np.where(vd.secondary_mask(nx, ny, rank, world), vis, np.float32(np.nan))
+    sbuf = torch.from_numpy(vd.pack_tiles_host(mine, rank, world))
+    assert sbuf.numel() == vrt.tiles_per_rank(vrt.Film(1, 1, nx, ny), world) * 64
+    sgl = [torch.empty_like(sbuf) for _ in range(world)] if rank == 0 else None
+    dist.gather(sbuf, sgl, dst=0)
     if rank == 0:
-        res["secondary"] = bool(np.array_equal(t.numpy().view(np.uint32), vis.view(np.uint32)))
+        svis = vd.unpack_tiles_host(torch.stack(sgl).numpy(), nx, ny, world, comps=1)
+        res["secondary"] = bool(np.array_equal(svis.view(np.uint32), vis.view(np.uint32)))
         with open(os.path.join(outdir, "res.json"), "w") as f:
             json.dump(res, f)
     dist.barrier()

@@ -2,9 +2,10 @@
 same protocol with oracle-rendered ranks): two gloo ranks sharing cuda:0,
 each rendering its share of the tile deal with vrt_render_tiles_device and
 its config-5 pixels with vrt_render_secondary_device; rank 0 gathers the
-packed tile buffers (gloo, host-staged), re-assembles them on the device with
-vrt_unpack_tiles_device, and sums the visibility parts -- both bit-exact vs
-the oracle's single-process images."""
+packed tile buffers (gloo, host-staged) and re-assembles them on the device
+with vrt_unpack_tiles_device; config 5's pixels take the same path with 1
+float per pixel (vrt_pack_tiles_c_device / vrt_unpack_tiles_c_device) --
+both bit-exact vs the oracle's single-process images."""
 import json
 import os
 import socket
@@ -51,18 +52,27 @@ def _worker(rank, world, port, outdir):
     host = buf.cpu()
     gl = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
     dist.gather(host, gl, dst=0)
-    # config 5: this rank's pixels of a zeroed visibility image, SUM reduce
+    # config 5: this rank's pixels (the rest of its image left as NaN), its
+    # tiles packed on the device (1 float per pixel) -> gather -> device
+    # unpack on rank 0, as the primary frame
     prim = torch.zeros(nx * ny * 8, dtype=torch.float32, device=dev)
-    part = torch.zeros((ny, nx), dtype=torch.float32, device=dev)
+    part = torch.full((ny, nx), float("nan"), dtype=torch.float32, device=dev)
     tree.render_secondary_device(cam, film, 4, rank, world, prim.data_ptr(), part.data_ptr(), None)
+    sbuf = torch.zeros(nt * 64, dtype=torch.float32, device=dev)
+    vrt.pack_tiles_c_device(film, rank, world, 1, part.data_ptr(), sbuf.data_ptr(), None)
     torch.cuda.synchronize()
-    t = part.cpu()
-    dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+    shost = sbuf.cpu()
+    sgl = [torch.empty_like(shost) for _ in range(world)] if rank == 0 else None
+    dist.gather(shost, sgl, dst=0)
     if rank == 0:
         g = torch.stack(gl).to(dev)
         img = torch.zeros((ny, nx, 3), dtype=torch.float32, device=dev)
         vrt.unpack_tiles_device(film, world, g.data_ptr(), img.data_ptr(), None)
+        sg = torch.stack(sgl).to(dev)
+        svis = torch.full((ny, nx), float("nan"), dtype=torch.float32, device=dev)
+        vrt.unpack_tiles_c_device(film, world, 1, sg.data_ptr(), svis.data_ptr(), None)
         torch.cuda.synchronize()
+        t = svis.cpu()
         osc = po.Scene(sd, depth)
         pcam = po.camera(fov, eye, spot, up)
         ref = osc.render(pcam, 1.0, 1.0, nx, ny, film_index=1, nthreads=2, samples=False)

@@ -11,7 +11,7 @@ from .api import (  # noqa: F401
     device_selftest_order,
     hdr_bytes, hdr_bytes_from_rgbe, intersect_triangle3, load_image, make_ray, obj2voxel, ray_march, ray_march_init,
     TEST_FORCE_DEFER, TEST_FAIL_LAUNCH, TEST_SPILL_ALL, TEST_STREAM_LEFTOVER, TEST_LIGHT_TAIL, TEST_PRIM_TAIL, TEST_SEC_DEFER, TEST_VIRTUAL_RANKS, render, set_test_flags, sweep_pose, tga_decode, tile_deal_map, tiles_per_rank, to_radian, tri_box_overlap,
-    unpack_tiles_device, write_hdr, rgbe_device, write_hdr_device,
+    unpack_tiles_device, pack_tiles_c_device, unpack_tiles_c_device, write_hdr, rgbe_device, write_hdr_device,
 )
 
 __all__ = [
@@ -19,6 +19,6 @@ __all__ = [
     "multi_tile_map",
     "device_count", "device_selftest", "hdr_bytes", "intersect_triangle3", "make_ray",
     "ray_march", "ray_march_init", "render", "sweep_pose", "tile_deal_map", "tiles_per_rank", "to_radian",
-    "tri_box_overlap", "unpack_tiles_device", "write_hdr", "ObjModel", "obj2voxel", "load_image",
+    "tri_box_overlap", "unpack_tiles_device", "pack_tiles_c_device", "unpack_tiles_c_device", "write_hdr", "ObjModel", "obj2voxel", "load_image",
     "tga_decode", "hdr_bytes_from_rgbe", "rgbe_device", "write_hdr_device", "build_id", "build_flag", "test_flags", "device_selftest_order", "set_test_flags",
 ]

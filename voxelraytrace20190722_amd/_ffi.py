@@ -110,6 +110,8 @@ SIGNATURES = {
     "vrt_render_tiles_device": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), C.c_int,
                                           C.c_int, C.c_int, _P, _P]),
     "vrt_unpack_tiles_device": (C.c_int, [C.POINTER(Film), C.c_int, _P, _P, _P]),
+    "vrt_pack_tiles_c_device": (C.c_int, [C.POINTER(Film), C.c_int, C.c_int, C.c_int, _P, _P, _P]),
+    "vrt_unpack_tiles_c_device": (C.c_int, [C.POINTER(Film), C.c_int, C.c_int, _P, _P, _P]),
     "vrt_last_kernel_ms": (C.c_int, [_P, f32p]),
     "vrt_render_secondary": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Film), C.c_int, f32p, i32p,
                                        i32p, u32p, i64p]),

@@ -619,6 +619,22 @@ def unpack_tiles_device(film, nranks, d_gathered_ptr, d_image_ptr, stream_ptr=No
           "vrt_unpack_tiles_device")
 
 
+def pack_tiles_c_device(film, rank, nranks, comps, d_image_ptr, d_packed_ptr, stream_ptr=None):
+    """Rank `rank`'s tiles of a (ny, nx, comps) device image -> its packed
+    buffer (vrt_pack_tiles_c_device; config 5: comps = 1)."""
+    check(lib().vrt_pack_tiles_c_device(C.byref(film.c), int(rank), int(nranks), int(comps), C.c_void_p(d_image_ptr),
+                                        C.c_void_p(d_packed_ptr), C.c_void_p(stream_ptr) if stream_ptr else None),
+          "vrt_pack_tiles_c_device")
+
+
+def unpack_tiles_c_device(film, nranks, comps, d_gathered_ptr, d_image_ptr, stream_ptr=None):
+    """Rank 0 after the gather: nranks packed buffers -> the (ny, nx, comps)
+    image (vrt_unpack_tiles_c_device)."""
+    check(lib().vrt_unpack_tiles_c_device(C.byref(film.c), int(nranks), int(comps), C.c_void_p(d_gathered_ptr),
+                                          C.c_void_p(d_image_ptr), C.c_void_p(stream_ptr) if stream_ptr else None),
+          "vrt_unpack_tiles_c_device")
+
+
 def intersect_triangle3(orig, direction, v0, v1, v2):
     """VRT/raytri.h:5-7 -> (ret, t, u, v); t/u/v only meaningful when ret == 1."""
     a = [np.ascontiguousarray(np.asarray(x, np.float64).reshape(3)) for x in (orig, direction, v0, v1, v2)]

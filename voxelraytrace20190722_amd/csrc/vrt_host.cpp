@@ -1610,6 +1610,30 @@ extern "C" int vrt_unpack_tiles_device(const vrt_film *film, int nranks,
         return VRT_OK;
 }
 
+extern "C" int vrt_pack_tiles_c_device(const vrt_film *film, int rank, int nranks, int comps, const float *d_image,
+                                       float *d_packed, void *stream)
+{
+        if (!d_image || !d_packed || nranks < 1 || rank < 0 || rank >= nranks || comps < 1 || comps > 4)
+                return fail(VRT_E_INVALID, "bad argument");
+        if (int rc = film_ok(film))
+                return rc;
+        HIPCHK(launch_pack_c(film->nx, film->ny, rank, nranks, comps, d_image, d_packed,
+                             static_cast<hipStream_t>(stream)));
+        return VRT_OK;
+}
+
+extern "C" int vrt_unpack_tiles_c_device(const vrt_film *film, int nranks, int comps, const float *d_gathered,
+                                         float *d_image, void *stream)
+{
+        if (!d_gathered || !d_image || nranks < 1 || comps < 1 || comps > 4)
+                return fail(VRT_E_INVALID, "bad argument");
+        if (int rc = film_ok(film))
+                return rc;
+        HIPCHK(launch_unpack_c(film->nx, film->ny, nranks, vrt_tiles_per_rank(film, nranks), comps, d_gathered,
+                               d_image, static_cast<hipStream_t>(stream)));
+        return VRT_OK;
+}
+
 extern "C" int vrt_rgbe_device(const float *d_img, int w, int h, int comp, uint8_t *d_rgbe, void *stream)
 {
         if (!d_img || !d_rgbe || w <= 0 || h <= 0 || comp < 1 || comp > 4)

@@ -519,6 +519,10 @@ hipError_t launch_ray_march(const DevScene &sc, const void *d_rays,
 hipError_t launch_unpack(int nx, int ny, int ntx, int nty, int nranks,
                          int tiles_per_rank, const float *src, float *dst,
                          hipStream_t st);
+hipError_t launch_pack_c(int nx, int ny, int rank, int nranks, int comps, const float *img, float *dst,
+                         hipStream_t st);
+hipError_t launch_unpack_c(int nx, int ny, int nranks, int tiles_per_rank, int comps, const float *src, float *dst,
+                           hipStream_t st);
 // q: the launch's work queue (persistent kernel) or nullptr (one wave per
 // pixel)
 hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,

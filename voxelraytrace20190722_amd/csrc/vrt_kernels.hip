@@ -2945,6 +2945,68 @@ __global__ void k_unpack4(int nx, int ny, int ntx, int nty, int nranks, int tpr,
         dst[i] = src[((int64_t)r * tpr + k) * 48 + (py & 7) * 6 + c];
 }
 
+// Any component count (config 5's visibility: 1 float per pixel): rank
+// rank's tiles of a (ny, nx, comps) image -> its packed buffer (tile k at
+// k * 64 * comps, pixels row-major inside the tile), and the gathered
+// buffers of every rank -> the image (zero outside the tile grid).  One
+// thread per float of the packed buffer / the image.
+__global__ void k_pack_c(int nx, int ntx, int nty, int rank, int nranks, int comps, int64_t n,
+                         const float *__restrict__ img, float *__restrict__ dst)
+{
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= n)
+                return;
+        const int64_t e = i / comps;
+        const int c = (int)(i % comps);
+        const int k = (int)(e >> 6), pp = (int)(e & 63);
+        int tx, ty;
+        deal_tile(tile_deal(ntx, nty, nranks), rank, k, tx, ty);
+        const int px = tx * 8 + (pp & 7), py = ty * 8 + (pp >> 3);
+        dst[i] = img[((int64_t)py * nx + px) * comps + c];
+}
+
+__global__ void k_unpack_c(int nx, int ny, int ntx, int nty, int nranks, int tpr, int comps,
+                           const float *__restrict__ src, float *__restrict__ dst)
+{
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= (int64_t)nx * ny * comps)
+                return;
+        const int64_t e = i / comps;
+        const int c = (int)(i % comps);
+        const int px = (int)(e % nx), py = (int)(e / nx);
+        const int tx = px >> 3, ty = py >> 3;
+        float v = 0.f;
+        if (tx < ntx && ty < nty) {
+                int r, k;
+                deal_slot(tile_deal(ntx, nty, nranks), tx, ty, r, k);
+                v = src[(((int64_t)r * tpr + k) * 64 + (py & 7) * 8 + (px & 7)) * comps + c];
+        }
+        dst[i] = v;
+}
+
+hipError_t launch_pack_c(int nx, int ny, int rank, int nranks, int comps, const float *img, float *dst,
+                         hipStream_t st)
+{
+        const int ntx = nx / 8, nty = ny / 8;
+        const int64_t n = (int64_t)deal_count(tile_deal(ntx, nty, nranks), rank) * 64 * comps;
+        if (n <= 0)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_pack_c, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nx, ntx, nty, rank,
+                           nranks, comps, n, img, dst);
+        return hipGetLastError();
+}
+
+hipError_t launch_unpack_c(int nx, int ny, int nranks, int tpr, int comps, const float *src, float *dst,
+                           hipStream_t st)
+{
+        const int64_t n = (int64_t)nx * ny * comps;
+        if (n <= 0)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_unpack_c, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nx, ny, nx / 8, ny / 8,
+                           nranks, tpr, comps, src, dst);
+        return hipGetLastError();
+}
+
 // Device copies of the MT / SAT leaves for bit-exact KATs.
 __global__ void k_selftest(const double *mt_in, double *mt_out,
                            const float *sat_in, int32_t *sat_out, int64_t n)

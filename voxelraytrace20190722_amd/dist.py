@@ -18,9 +18,11 @@ nranks, F = whole blocks).  A rank's k-th tile: its blocks' tiles first
 (block order, row-major inside a block), then its leftover tiles.  A rank's
 buffer holds its tiles in that order, 64 pixels each, row-major inside the
 tile, 3 floats per pixel, `tiles_per_rank * 192` floats (the largest share;
-unused tail zero).  Secondary frames (config 5): the same deal; every rank
-writes only the pixels of its tiles into a zeroed image, so a SUM reduce
-re-assembles it exactly.
+unused tail zero).  Secondary frames (config 5): the same deal and the same
+packed layout with 1 float per pixel (`tiles_per_rank * 64` floats): every
+rank renders its pixels, packs its tiles (vrt_pack_tiles_c_device), one
+gather brings the buffers to rank 0, which re-assembles the visibility image
+(vrt_unpack_tiles_c_device) -- the primary frame's collective.
 """
 import numpy as np
 
@@ -93,29 +95,32 @@ def rank_tiles(nx, ny, rank, nranks, g=None):
 
 
 def pack_tiles_host(img, rank, nranks, g=None):
-    """This rank's packed tile buffer from a full (ny, nx, 3) image."""
+    """This rank's packed tile buffer from a full (ny, nx, 3) image, or from a
+    (ny, nx) / (ny, nx, c) image of c floats per pixel (== vrt_pack_tiles_c_device)."""
     ny, nx = img.shape[:2]
+    c = 1 if img.ndim == 2 else img.shape[2]
     ntx, _ = tile_grid(nx, ny)
     tpr = tiles_per_rank(nx, ny, nranks, g)
-    buf = np.zeros((tpr, 64, 3), np.float32)
+    buf = np.zeros((tpr, 64, c), np.float32)
     for k, t in enumerate(rank_tiles(nx, ny, rank, nranks, g)):
         tx, ty = t % ntx, t // ntx
-        buf[k] = img[ty * 8:ty * 8 + 8, tx * 8:tx * 8 + 8].reshape(64, 3)
+        buf[k] = img[ty * 8:ty * 8 + 8, tx * 8:tx * 8 + 8].reshape(64, c)
     return buf.reshape(-1)
 
 
-def unpack_tiles_host(gathered, nx, ny, nranks, g=None):
-    """== vrt_unpack_tiles_device: (nranks, tiles_per_rank*192) -> (ny, nx, 3);
-    pixels outside the tile grid are zero."""
+def unpack_tiles_host(gathered, nx, ny, nranks, g=None, comps=3):
+    """== vrt_unpack_tiles_device (comps = 3) / vrt_unpack_tiles_c_device:
+    (nranks, tiles_per_rank*64*comps) -> (ny, nx, comps), (ny, nx) for
+    comps = 1; pixels outside the tile grid are zero."""
     ntx, nty = tile_grid(nx, ny)
     tpr = tiles_per_rank(nx, ny, nranks, g)
     rk, sl, _ = deal_owner(nx, ny, nranks, g)
-    gg = np.asarray(gathered, np.float32).reshape(nranks, tpr, 8, 8, 3)
-    img = np.zeros((ny, nx, 3), np.float32)
+    gg = np.asarray(gathered, np.float32).reshape(nranks, tpr, 8, 8, comps)
+    img = np.zeros((ny, nx, comps), np.float32)
     for ty in range(nty):
         for tx in range(ntx):
             img[ty * 8:ty * 8 + 8, tx * 8:tx * 8 + 8] = gg[rk[ty, tx], sl[ty, tx]]
-    return img
+    return img[:, :, 0] if comps == 1 else img
 
 
 def secondary_mask(nx, ny, rank, nranks, g=None):
