@@ -405,7 +405,8 @@ def test_secondary_compaction_matches_oracle(proxy_small, depth, flags, spp):
     assert np.array_equal(bits(vis), bits(ovis))
     assert vrt.build_flag("VRT_SEC_SPILL_T") > 0  # the compaction is built in
     if flags & vrt.TEST_SPILL_ALL:  # every wave stops at its first ended ray: most rays are saved
-        assert counts[0] > rays // 20, (counts, rays)
+        # (of the pixels the fast-only kernel walks: half of them with TEST_SEC_DEFER)
+        assert counts[0] > rays // (40 if flags & vrt.TEST_SEC_DEFER else 20), (counts, rays)
     # the one streaming resume round walks every saved ray to its end: no
     # later queue is ever filled
     assert counts[1:] == [0, 0, 0], counts
