@@ -42,7 +42,7 @@ def main():
     film = _ffi.Film(1.0, 1.0, a.width, a.height)
     img = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device="cuda:0")
     st = torch.cuda.current_stream()
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 24)()
     cams = []
     for i in range(a.poses):
         fov, eye, spot, up = vrt.sweep_pose(info.root_min[:], info.root_max[:], i, a.poses)
@@ -71,6 +71,12 @@ def main():
         "cycles_per_unit": g[10] / n, "cycles_inner_frac": g[8] / max(1, g[10]),
         "cycles_leaf_frac": g[9] / max(1, g[10]),
         "cycles_other_frac": 1 - (g[8] + g[9]) / max(1, g[10]),
+        # wave iterations of the node-visit loop per unit (ray-wave) in which
+        # some lane does X: the blocks X runs issue once per such iteration
+        "visit_iters_per_unit": g[12] / n, "pop_iters_per_unit": g[13] / n,
+        "linebox_skip_iters_per_unit": g[14] / n, "expand_iters_per_unit": g[15] / n,
+        "order2_iters_per_unit": g[16] / n, "rank8_iters_per_unit": g[17] / n,
+        "net4_iters_per_unit": g[18] / n, "leaf_stop_iters_per_unit": g[19] / n,
     }
     print(json.dumps({k: round(v, 4) if isinstance(v, float) else v for k, v in out.items()}, indent=1))
 

@@ -1171,17 +1171,15 @@ extern "C" int vrt_tiles_per_rank(const vrt_film *film, int nranks)
         return m;
 }
 
-#ifndef VRT_INFLIGHT_GRID_DIV
-#define VRT_INFLIGHT_GRID_DIV 2
-#endif
 extern "C" int vrt_scene_set_frames_in_flight(vrt_scene *s, int n)
 {
         if (!s || n < 1)
                 return fail(VRT_E_INVALID, "bad argument");
         std::lock_guard<std::mutex> lk(s->mu);
         // measured: half the slots per frame with 2-3 frames
-        // in flight; a third is slower
-        s->dev.grid_div = n >= 2 ? VRT_INFLIGHT_GRID_DIV : 1;
+        // in flight; a third is slower, the whole chip per frame the same
+        // (round 6, bench's own schedule)
+        s->dev.grid_div = n >= 2 ? 2 : 1;
         return VRT_OK;
 }
 

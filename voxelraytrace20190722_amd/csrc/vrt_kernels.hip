@@ -150,7 +150,22 @@ __device__ uint32_t g_unit_diag[kUnitDiagMax * 4];
 __device__ uint32_t g_unit_walk[kUnitDiagMax * 4];  // with VRT_LIGHT_DIAG: wave max / sum of node visits, triangle tests
 #endif
 #if VRT_PHASE_STAMPS
-__device__ unsigned long long g_phase[16];
+// [0..11] per-wave phase totals (ray_march); [12..19] wave iterations of the
+// node-visit loop in which some lane: [12] iterates at all, [13] pops a stack
+// entry, [14] is skipped by the triangle-box line test, [15] expands an
+// internal node, [16] orders >= 2 hit children, [17] > 4 (rank_order8),
+// [18] 3-4 (net4_order) with none > 4, [19] stops at a leaf
+constexpr int kPhaseWords = 24;
+__device__ unsigned long long g_phase[kPhaseWords];
+// counted by the first active lane of the wave only: summed over the
+// lanes, each wave iteration counts once
+__device__ __forceinline__ uint32_t wave_lead()
+{
+        const uint64_t act = __ballot(1);
+        int lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        return (uint32_t)lane == (uint32_t)(__ffsll((long long)act) - 1) ? 1u : 0u;
+}
 #endif
 
 // ---------------------------------------------------------------------------
@@ -861,6 +876,7 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
 #if VRT_PHASE_STAMPS
         uint32_t d_it = 0, d_lp = 0, d_tri = 0, d_lpmax = 0, d_lpsum = 0, d_phmax = 0;
         unsigned long long d_tin = 0, d_tleaf = 0;
+        uint32_t d_ev[8] = {};  // g_phase[12..19], counted by the wave's first active lane
 #endif
         // VRT_LIGHT_DIAG builds: node visits, leaf phases and triangle tests
         // of this lane's walk, into m.A / m.L / m.T
@@ -874,6 +890,11 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                 for (;;) {
 #if VRT_PHASE_STAMPS
                         ++d_it;
+                        {
+                                const uint32_t ld = wave_lead();
+                                d_ev[0] += ld;
+                                d_ev[1] += ld & (__ballot(cnt == 0 && sp > 0) != 0ull);
+                        }
 #endif
                         if (VRT_LIGHT_DIAG)
                                 ++dg_it;
@@ -904,11 +925,18 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         if (kNB) {
                                 float tmn[3], tmx[3];
                                 load_xnode(sc.xnodes, node, bmin, bmax, a, b, tmn, tmx);
-                                if (lbok && !line_meets_box(tmn, tmx, r))
+                                const bool skip = lbok && !line_meets_box(tmn, tmx, r);
+#if VRT_PHASE_STAMPS
+                                d_ev[2] += wave_lead() & (__ballot(skip) != 0ull);
+#endif
+                                if (skip)
                                         continue;  // no triangle below this node can pass
                         } else {
                                 load_node(nodes, node, bmin, bmax, a, b);
                         }
+#if VRT_PHASE_STAMPS
+                        d_ev[7] += wave_lead() & (__ballot((a & kLeafBit) != 0u) != 0ull);
+#endif
                         if (!(a & kLeafBit)) {
                                 if (cnt) {
                                         stk[sp * kS] = make_uint2(base, order | ((uint32_t)cnt << 24));
@@ -917,6 +945,16 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                                         ++sp;
                                 }
                                 order = expand<kCount, kFast, kStd>(bmin, bmax, r, cnt, fpos, kCount ? 0xFFu : b);
+#if VRT_PHASE_STAMPS
+                                {
+                                        const uint32_t ld = wave_lead();
+                                        d_ev[3] += ld;
+                                        d_ev[4] += ld & (__ballot(cnt >= 2) != 0ull);
+                                        const bool big = __ballot(cnt > 4) != 0ull;
+                                        d_ev[5] += ld & big;
+                                        d_ev[6] += ld & !big & (__ballot(cnt >= 3) != 0ull);
+                                }
+#endif
                                 base = a;
                                 ++depth;
                                 ++nexp;
@@ -1003,6 +1041,12 @@ __device__ __forceinline__ void ray_march(const DevScene &sc, const RayK &r,
                         atomicAdd(&g_phase[8], tin);
                         atomicAdd(&g_phase[9], tleaf);
                         atomicAdd(&g_phase[11], 1ull);
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                        const uint32_t t = wave_sum_u32(d_ev[e]);
+                        if ((threadIdx.x & 63) == 0)
+                                atomicAdd(&g_phase[12 + e], (unsigned long long)t);
                 }
         }
 #endif
@@ -2445,6 +2489,13 @@ __device__ __forceinline__ bool stream_chunk_fast(const ResumeParams &p, const S
         return __all(ok);
 }
 
+// resume_stream tests its lanes' leaves once at least this many hold one
+// (or no idle lane can get more work); 0: every turn
+#ifndef VRT_STREAM_LEAF_T
+#define VRT_STREAM_LEAF_T 32
+#endif
+constexpr uint32_t kStreamLeafT = VRT_STREAM_LEAF_T;
+
 template <bool kR64>
 __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *cin, uint32_t nch,
                                               const uint32_t *fins, const SpillRec *in, uint2 *stk,
@@ -2463,6 +2514,8 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
         bool busy = false;
         uint32_t slot = lane, base = 0, mask = 0, s = 0;
         int sp = 0, bot = 0;
+        bool leaf = false;  // this lane holds a leaf (b, nref) not yet tested
+        uint32_t nref = 0, b = 0;
         RayK r;
         r.o = r.d = r.dinv = mk3(0.f, 0.f, 0.f);
         r.tmin = p.res;
@@ -2471,6 +2524,26 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
                 *hword = 0ull;
         wave_lds_sync();
         for (;;) {
+                // 0. slots no lane walks any more have ended (their pieces all
+                // walked, or a hit): report and free them
+                const uint64_t live = wave_or_u64(busy ? 1ull << slot : 0ull);
+                const uint64_t done = assigned & ~live;
+                if (done != 0ull) {
+                        const uint64_t hm = *hword;
+                        if ((done >> lane) & 1ull) {
+                                const uint32_t inf = sinfo[lane];
+                                const uint32_t pix = inf & 0x3FFFFFFu, smp = inf >> 26;
+                                const uint32_t vi = (pix / (uint32_t)p.W8) * (uint32_t)p.nx + pix % (uint32_t)p.W8;
+                                const uint32_t h = (uint32_t)((hm >> lane) & 1ull);
+                                if (p.s_hit)
+                                        p.s_hit[(size_t)vi * (size_t)p.spp + smp] = (int32_t)h;
+                                float *pr = p.prim + 8 * (size_t)pix;
+                                const uint32_t old = atomicAdd(reinterpret_cast<uint32_t *>(pr) + 7, h ? 255u : 0xFFFFFFFFu);
+                                if ((old & 0xFFu) == 1u)  // the pixel's last ray
+                                        p.vis[vi] = (float)(p.spp - (int)((old >> 8) + h)) / spp_f(p.spp);
+                        }
+                        assigned &= ~done;
+                }
                 // 1. hand pieces to idle lanes
                 uint64_t idle = __ballot(!busy);
                 const bool spare = busy && (sp > bot || __popc(mask) >= 2);
@@ -2581,10 +2654,9 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
                         if (cur >= fill)
                                 continue;  // take the next chunk
                 }
-                // 3. every busy lane: advance to its next leaf and test it (occl_walk)
-                bool leaf = false;
-                uint32_t nref = 0, b = 0;
-                if (busy) {
+                // 3. every busy lane without a leaf in hand: advance to its next
+                // leaf (occl_walk); a lane holding one from an earlier turn keeps it
+                if (busy && !leaf) {
                         float bmin[3], bmax[3];
                         uint32_t a;
                         for (;;) {
@@ -2624,6 +2696,16 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
                                 sp = bot = 0;
                         }
                 }
+                // 4. the leaf tests, together: while fewer than kStreamLeafT
+                // lanes hold a leaf and idle lanes can still get work (a
+                // donor with a piece to spare, or more saved rays), the
+                // holders wait and the others take work and advance first, so
+                // the MT loop runs on more lanes at a time (which leaves are
+                // tested when does not change a slot's OR of hits)
+                const uint64_t lm = __ballot(leaf);
+                if (lm != 0ull && (uint32_t)__popcll(lm) < kStreamLeafT && lm != ~0ull &&
+                    (more || __ballot(leaf && (sp > bot || __popc(mask) >= 2)) != 0ull))
+                        continue;
                 bool hit = false;
                 if (leaf) {
                         bool done = false;
@@ -2637,6 +2719,7 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
                         }
                         if (!done)
                                 hit = leaf_any<kR64>(sc.refs, b, nref, r);
+                        leaf = false;
                 }
                 if (__ballot(hit) != 0ull) {
                         if (hit)
@@ -2648,25 +2731,6 @@ __device__ __forceinline__ void resume_stream(const ResumeParams &p, uint32_t *c
                                 mask = 0;
                                 sp = bot = 0;
                         }
-                }
-                // 4. slots no lane walks any more have ended: report and free them
-                const uint64_t live = wave_or_u64(busy ? 1ull << slot : 0ull);
-                const uint64_t done = assigned & ~live;
-                if (done != 0ull) {
-                        const uint64_t hm = *hword;
-                        if ((done >> lane) & 1ull) {
-                                const uint32_t inf = sinfo[lane];
-                                const uint32_t pix = inf & 0x3FFFFFFu, smp = inf >> 26;
-                                const uint32_t vi = (pix / (uint32_t)p.W8) * (uint32_t)p.nx + pix % (uint32_t)p.W8;
-                                const uint32_t h = (uint32_t)((hm >> lane) & 1ull);
-                                if (p.s_hit)
-                                        p.s_hit[(size_t)vi * (size_t)p.spp + smp] = (int32_t)h;
-                                float *pr = p.prim + 8 * (size_t)pix;
-                                const uint32_t old = atomicAdd(reinterpret_cast<uint32_t *>(pr) + 7, h ? 255u : 0xFFFFFFFFu);
-                                if ((old & 0xFFu) == 1u)  // the pixel's last ray
-                                        p.vis[vi] = (float)(p.spp - (int)((old >> 8) + h)) / spp_f(p.spp);
-                        }
-                        assigned &= ~done;
                 }
         }
 }
@@ -3933,8 +3997,9 @@ __device__ __forceinline__ f3 cone_march_axes(const TraceParams &p, f3 o, f3 d, 
         f3 diffuse = mk3(0.f, 0.f, 0.f);
         // the last descent's cell
         f3 lo = mk3(0.f, 0.f, 0.f), hi = lo;
-        int c_level = -1, c_split = 0;
-        uint32_t c_ni = 0;
+        int c_level = -1;
+        // the last descent's node: its coverage (+0 when the descent ended
+        // above the split level: the step adds nothing) and illumination
         float cov = 0.f;
         f3 il = mk3(0.f, 0.f, 0.f);
         // (constant address space, index the same in every active lane: the
@@ -3946,21 +4011,17 @@ __device__ __forceinline__ f3 cone_march_axes(const TraceParams &p, f3 o, f3 d, 
                 const float dist = tab[ku], inv = tab[ku + 1];
                 const int level = __float_as_int(tab[ku + 2]);
                 const f3 pt = o + d * dist;
-                int split = level;
-                uint32_t ni = 0;
-                bool same = false;
-                if (level == c_level && pt.x > lo.x && pt.x <= hi.x && pt.y > lo.y && pt.y <= hi.y &&
-                    pt.z > lo.z && pt.z <= hi.z) {
-                        split = c_split;
-                        ni = c_ni;
-                        same = true;
-                } else {
-                        uint32_t a = a0;
-                        float4 c = c0;
+                // one divergent region per step: the cell test without
+                // short-circuit branches (& of the compares)
+                const bool same = (level == c_level) & (pt.x > lo.x) & (pt.x <= hi.x) & (pt.y > lo.y) &
+                                  (pt.y <= hi.y) & (pt.z > lo.z) & (pt.z <= hi.z);
+                if (!same) {
+                        int split = level;
+                        uint32_t ni = 0, a = a0;
                         int i = octant_of(pt, c0);
                         while (!(a & kLeafBit) && split) {
                                 ni = a + (uint32_t)i;
-                                c = p.cc[ni];
+                                const float4 c = p.cc[ni];
                                 a = __float_as_uint(c.w);
                                 i = octant_of(pt, c);
                                 split--;
@@ -3970,45 +4031,41 @@ __device__ __forceinline__ f3 cone_march_axes(const TraceParams &p, f3 o, f3 d, 
                         lo = mk3(l4.x, l4.y, l4.z);
                         hi = mk3(h4.x, h4.y, h4.z);
                         c_level = level;
-                        c_split = split;
-                        c_ni = ni;
-                }
-                if (split == 0) {
-                        if (!same) {  // (the same node's cov and il are still held)
-                                const LMRec *R = p.lm + ni;
-                                float L[9];
-                                cov = R->cov;
+                        // the node's light-map entry (a valid node also when the
+                        // descent ended at a leaf above the split level, whose
+                        // coverage is then taken as +0)
+                        const LMRec *R = p.lm + ni;
+                        float L[9];
+                        float cv = R->cov;
 #pragma unroll
-                                for (int k = 0; k < 3; ++k) {
-                                        L[k] = R->illum[3 * jx + k];
-                                        L[3 + k] = R->illum[3 * jy + k];
-                                        L[6 + k] = R->illum[3 * jz + k];
-                                }
-                                // the 10 loads issue together (not sunk into the branch)
-                                asm volatile("" : "+v"(cov), "+v"(L[0]), "+v"(L[1]), "+v"(L[2]), "+v"(L[3]),
-                                             "+v"(L[4]), "+v"(L[5]), "+v"(L[6]), "+v"(L[7]), "+v"(L[8]));
-                                if (cov != 0.f) {
-                                        const f3 tx = mk3(cx * L[0], cx * L[1], cx * L[2]);
-                                        const f3 ty = mk3(cy * L[3], cy * L[4], cy * L[5]);
-                                        const f3 tz = mk3(cz * L[6], cz * L[7], cz * L[8]);
-                                        const f3 z0 = mk3(0.f, 0.f, 0.f);
-                                        il = z0;
-                                        il = il + (jx == 0 ? tx : z0);
-                                        il = il + (jy == 1 ? ty : z0);
-                                        il = il + (jz == 2 ? tz : z0);
-                                        il = il + (jx == 3 ? tx : z0);
-                                        il = il + (jy == 4 ? ty : z0);
-                                        il = il + (jz == 5 ? tz : z0);
-                                }
+                        for (int q = 0; q < 3; ++q) {
+                                L[q] = R->illum[3 * jx + q];
+                                L[3 + q] = R->illum[3 * jy + q];
+                                L[6 + q] = R->illum[3 * jz + q];
                         }
-                        if (cov != 0.f) {
-                                const float transparency = clampf(1.f - opacity, 0.f, 1.f);
-                                const float aa = cov * step;
-                                const float w = inv * transparency * cov;  // inv = 1 / (1 + decay * dist)
-                                diffuse = mk3(diffuse.x + w * il.x, diffuse.y + w * il.y, diffuse.z + w * il.z);
-                                opacity += transparency * aa;
-                        }
+                        cov = split == 0 ? cv : 0.f;
+                        const f3 tx = mk3(cx * L[0], cx * L[1], cx * L[2]);
+                        const f3 ty = mk3(cy * L[3], cy * L[4], cy * L[5]);
+                        const f3 tz = mk3(cz * L[6], cz * L[7], cz * L[8]);
+                        const f3 z0 = mk3(0.f, 0.f, 0.f);
+                        il = z0;
+                        il = il + (jx == 0 ? tx : z0);
+                        il = il + (jy == 1 ? ty : z0);
+                        il = il + (jz == 2 ? tz : z0);
+                        il = il + (jx == 3 ? tx : z0);
+                        il = il + (jy == 4 ? ty : z0);
+                        il = il + (jz == 5 ? tz : z0);
                 }
+                // branch-free: with cov = +0 (coverage zero, or no node at the
+                // split level) w = +0 and transparency * aa = +0, and w * il is
+                // +-0 for the finite il of a finite light map, so diffuse and
+                // opacity keep their values bit for bit (they start at +0 and
+                // never become -0), exactly as the reference's skipped step
+                const float transparency = clampf(1.f - opacity, 0.f, 1.f);
+                const float aa = cov * step;
+                const float w = inv * transparency * cov;  // inv = 1 / (1 + decay * dist)
+                diffuse = mk3(diffuse.x + w * il.x, diffuse.y + w * il.y, diffuse.z + w * il.z);
+                opacity += transparency * aa;
         }
         return diffuse;
 }
@@ -4460,12 +4517,13 @@ bool build_flag(const char *name, int64_t *value)
 }  // namespace vrt
 
 #if VRT_PHASE_STAMPS
-extern "C" __attribute__((visibility("default"))) int vrt_diag_phases(unsigned long long out[16], int reset)
+extern "C" __attribute__((visibility("default"))) int vrt_diag_phases(unsigned long long out[24], int reset)
 {
-        if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_phase), sizeof(unsigned long long) * 16) != hipSuccess)
+        if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_phase), sizeof(unsigned long long) * vrt::kPhaseWords) !=
+            hipSuccess)
                 return -1;
         if (reset) {
-                unsigned long long z[16] = {};
+                unsigned long long z[vrt::kPhaseWords] = {};
                 if (hipMemcpyToSymbol(HIP_SYMBOL(vrt::g_phase), z, sizeof z) != hipSuccess)
                         return -1;
         }
