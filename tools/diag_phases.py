@@ -78,6 +78,11 @@ def main():
         "order2_iters_per_unit": g[16] / n, "rank8_iters_per_unit": g[17] / n,
         "net4_iters_per_unit": g[18] / n, "leaf_stop_iters_per_unit": g[19] / n,
     }
+    # a persistent wave's time per unit: dequeue, setup (tile, ray, vote),
+    # the march call (root + walk), shading + film store
+    span = max(1, g[20] + g[21] + g[22] + g[23])
+    out.update({"unit_cycles_wave": span / n, "dequeue_frac": g[20] / span, "setup_frac": g[21] / span,
+                "march_frac": g[22] / span, "shade_store_frac": g[23] / span})
     print(json.dumps({k: round(v, 4) if isinstance(v, float) else v for k, v in out.items()}, indent=1))
 
 

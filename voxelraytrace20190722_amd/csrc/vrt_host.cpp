@@ -945,6 +945,8 @@ extern "C" int vrt_scene_create_ex(const vrt_scene_desc *d, int max_depth,
                         s->texs[t].c = d->tex_dims[3 * t + 2];
                         s->texs[t].pad = 0;
                 }
+                for (auto &mr : s->mats)
+                        mr.tx = (mr.tex >= 0 && mr.tex < d->ntex) ? s->texs[(size_t)mr.tex] : TexRec{};
                 s->tex_bytes = d->ntex ? d->tex_bytes : 0;
         } catch (const std::bad_alloc &) {
                 return fail(VRT_E_NOMEM, "octree build: out of host memory");

@@ -77,15 +77,20 @@ struct alignas(16) TriPos {
         float pad[3];
 };
 
-struct alignas(16) MatRec {
-        int32_t tex;  // -1 = untextured: Kd
-        float kd[3];
-};
-
 struct alignas(16) TexRec {
         int64_t off;
         int32_t w, h, c, pad;
 };
+
+// A material with its texture's record inline (a copy of texs[tex]), so a
+// textured hit's shading is TriAttr (beside TriPos) -> MatRec -> texel: one
+// dependent load fewer than MatRec -> TexRec.
+struct alignas(16) MatRec {
+        int32_t tex;  // -1 = untextured: Kd
+        float kd[3];
+        TexRec tx;    // texs[tex] when tex >= 0, else zero
+};
+static_assert(sizeof(MatRec) == 48, "MatRec must be 48 B");
 
 // Device-side scene view passed by value to kernels.
 struct DevScene {

@@ -154,7 +154,11 @@ __device__ uint32_t g_unit_walk[kUnitDiagMax * 4];  // with VRT_LIGHT_DIAG: wave
 // node-visit loop in which some lane: [12] iterates at all, [13] pops a stack
 // entry, [14] is skipped by the triangle-box line test, [15] expands an
 // internal node, [16] orders >= 2 hit children, [17] > 4 (rank_order8),
-// [18] 3-4 (net4_order) with none > 4, [19] stops at a leaf
+// [18] 3-4 (net4_order) with none > 4, [19] stops at a leaf; cycles of the
+// persistent render per unit (wave lead): [20] the dequeue (take_unit),
+// [21] render_unit's entry to the march call (tile, ray, fast-path vote),
+// [22] the march call (ray_march: root + walk), [23] the march's return to
+// render_unit's end (shading, film sum and store)
 constexpr int kPhaseWords = 24;
 __device__ unsigned long long g_phase[kPhaseWords];
 // counted by the first active lane of the wave only: summed over the
@@ -1710,6 +1714,10 @@ __device__ __forceinline__ f3 hit_albedo(const DevScene &sc, const MarchResult &
         const TriAttr *ta = sc.tri_attr + m.tri;
         const float4 *q = reinterpret_cast<const float4 *>(ta);
         const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+        // the vertices (textured materials only) are loaded beside the
+        // attributes, not after the material that says they are needed
+        const float4 *pp = reinterpret_cast<const float4 *>(sc.tri_pos + m.tri);
+        const float4 p0 = pp[0], p1 = pp[1], p2 = pp[2];
         const f3 n0 = mk3(a0.x, a0.y, a0.z), n1 = mk3(a0.w, a1.x, a1.y),
                  n2 = mk3(a1.z, a1.w, a2.x);
         const float t0u = a2.y, t0v = a2.z, t1u = a2.w, t1v = a3.x,
@@ -1722,8 +1730,6 @@ __device__ __forceinline__ f3 hit_albedo(const DevScene &sc, const MarchResult &
         if (mr.tex < 0) {
                 albedo = mk3(mr.kd[0], mr.kd[1], mr.kd[2]);
         } else {
-                const float4 *pp = reinterpret_cast<const float4 *>(sc.tri_pos + m.tri);
-                const float4 p0 = pp[0], p1 = pp[1], p2 = pp[2];
                 f3 bc = barycentric(m.hp, mk3(p0.x, p0.y, p0.z),
                                     mk3(p0.w, p1.x, p1.y),
                                     mk3(p1.z, p1.w, p2.x));
@@ -1732,7 +1738,7 @@ __device__ __forceinline__ f3 hit_albedo(const DevScene &sc, const MarchResult &
                 bc.z = clampf(bc.z, 0.f, 1.f);
                 const float tu = (bc.x * t0u + bc.y * t1u) + bc.z * t2u;
                 const float tv = (bc.x * t0v + bc.y * t1v) + bc.z * t2v;
-                const TexRec tx = sc.texs[mr.tex];
+                const TexRec tx = mr.tx;  // texs[mr.tex], inline
                 const int x = clampi((int)(unit_cycle(tu) * (float)tx.w), 0, tx.w - 1);
                 int y = clampi((int)(unit_cycle(tv) * (float)tx.h), 0, tx.h - 1);
                 y = tx.h - 1 - y;
@@ -1783,6 +1789,9 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
                 return l;
         };
+#if VRT_PHASE_STAMPS
+        const unsigned long long d_r0 = __builtin_amdgcn_s_memtime();
+#endif
         const CamParams &c = p.cam;
         int tx, ty;
         {
@@ -1826,10 +1835,23 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]), dn, c.tmin, c.tmax);
 
         MarchResult m;
+#if VRT_PHASE_STAMPS
+        unsigned long long d_m1 = 0;
+#endif
         if (kFastOnly) {
                 if (!wave_fast_std(p.sc, r) || (p.test_flags & VRT_TEST_FORCE_DEFER))
                         return false;
+#if VRT_PHASE_STAMPS
+                const unsigned long long d_m0 = __builtin_amdgcn_s_memtime();
+                if (lane_now() == 0)
+                        atomicAdd(&g_phase[21], d_m0 - d_r0);
+#endif
                 ray_march<false, true, kS, kFastStd, true, kR64>(p.sc, r, stk, nullptr, nullptr, m);
+#if VRT_PHASE_STAMPS
+                d_m1 = __builtin_amdgcn_s_memtime();
+                if (lane_now() == 0)
+                        atomicAdd(&g_phase[22], d_m1 - d_m0);
+#endif
         } else {
                 ray_march_dispatch<kCount, kS, true, kR64>(p.sc, r, stk, stk_aux, path_rem, m);
         }
@@ -1898,6 +1920,10 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                 o[1] = acc[1];
                 o[2] = acc[2];
         }
+#if VRT_PHASE_STAMPS
+        if (kFastOnly && lane_now() == 0)
+                atomicAdd(&g_phase[23], __builtin_amdgcn_s_memtime() - d_m1);
+#endif
         return true;
 }
 
@@ -1991,7 +2017,14 @@ __global__ __launch_bounds__(kPersistBlock, VRT_PERSIST_WAVES_PER_EU) void k_ren
                 if (n <= 0)
                         continue;
                 for (;;) {
+#if VRT_PHASE_STAMPS
+                        const unsigned long long d_q0 = __builtin_amdgcn_s_memtime();
+#endif
                         const uint32_t u = take_unit(p.q.ctr + x * kQueueStride) - p.q.base[x];
+#if VRT_PHASE_STAMPS
+                        if (lane == 0)
+                                atomicAdd(&g_phase[20], __builtin_amdgcn_s_memtime() - d_q0);
+#endif
                         if (u >= (uint32_t)n)
                                 break;
                         const int kq = slice_unit(units, x, (int)u, VRT_SLICE_CHUNK);
