@@ -1024,8 +1024,7 @@ def main():
     ref_bytes, per_ray = None, None
     if not a.no_counters and not rehearse and not secondary and not trace:
         poses_used = sorted({k % a.poses for k in range(a.steps)})
-        b_rank = []
-        cnt_tot = np.zeros(4)
+        b_rank, cnt_pose = [], {}
         for pi in poses_used:
             _, so = tree.render(cams[pi], film, counters=True)
             c = so["counters"].reshape(a.height, a.width, 4, 4)
@@ -1037,7 +1036,7 @@ def main():
             mask = np.repeat(np.repeat(m, 8, 0), 8, 1)
             cc = c[:H8, :W8][mask].reshape(-1, 4).astype(np.float64)
             s = cc.sum(0)
-            cnt_tot += s
+            cnt_pose[pi] = s
             npx = mask.sum()
             b_rank.append(28 * s[0] + 8 * s[1] + 40 * s[2] + 68 * s[3] + 12 * npx)
         pose_b = dict(zip(poses_used, b_rank))
@@ -1046,7 +1045,9 @@ def main():
         # design loads (child boxes are derived, never loaded) -- reported,
         # never divided by the HBM peak
         ref_bytes = round(float(np.mean([pose_b[k % a.poses] for k in range(a.steps)])))
-        nr = cnt_tot / (len(poses_used) * rays_per_frame / world)
+        # per ray over the same timed frames (a pose counted as often as it
+        # is rendered), so ref_bytes = the model applied to these counters
+        nr = np.mean([cnt_pose[k % a.poses] for k in range(a.steps)], axis=0) / (rays_per_frame / world)
         per_ray = {"A": round(float(nr[0]), 2), "L": round(float(nr[1]), 2),
                    "T": round(float(nr[2]), 2), "H": round(float(nr[3]), 3)}
     trace_kernels = None

@@ -1,5 +1,6 @@
 #!/bin/bash
-# The measurement set of a round in one GPU call: GPU tests, smoke, the C2 /
+# The measurement set of a round in one GPU call: GPU tests, smoke, the
+# driver's own bench command (bench.py --gpus 1 --steps 20 --warmup 5), the C2 /
 # C3 / config-5 / trace bench lines with their PMC passes and kernel-trace
 # stats saved (bench.py --pmc-save), the 8/4/2-rank RCCL rehearsals and a
 # 2-rank gloo run of the spawning launcher.  tools/save_profiles.sh TAG then
@@ -9,6 +10,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 rm -rf gpurun_out/pmc_bench gpurun_out/pmc_4k gpurun_out/pmc_sec gpurun_out/pmc_trace
 B="python -u bench.py"
 exec bash tools/check_call.sh "$@" \
+  "drv|500|$B --gpus 1 --steps 20 --warmup 5" \
   "bench|500|$B --pmc-save gpurun_out/pmc_bench" \
   "bench_4k|500|$B --width 3840 --height 2160 --depth 9 --pmc-save gpurun_out/pmc_4k" \
   "bench_sec|700|$B --mode secondary --pmc-save gpurun_out/pmc_sec" \
