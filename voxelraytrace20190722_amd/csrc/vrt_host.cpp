@@ -376,6 +376,8 @@ struct vrt_scene {
         hipEvent_t spill_ev[2] = {};
         bool spill_live[2] = {};
         hipStream_t spill_stream[2] = {};  // the set's last user (a stream keeps its set)
+        // per set: the side stream of its deferred-pixel walk, fork / join
+        SideLaunch spill_side[2] = {};
         uint32_t *h_spill = nullptr;       // pinned: per set, its last launch's round counters (ctr[0..7])
         uint32_t spill_want = 0;           // queue-0 chunks the next launch sizes for (0: first estimate)
         int spill_next = 0;
@@ -1049,6 +1051,12 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                                 (void)hipFree(s->d_spill[k]);
                         if (s->spill_ev[k])
                                 (void)hipEventDestroy(s->spill_ev[k]);
+                        if (s->spill_side[k].st)
+                                (void)hipStreamDestroy(s->spill_side[k].st);
+                        if (s->spill_side[k].fork)
+                                (void)hipEventDestroy(s->spill_side[k].fork);
+                        if (s->spill_side[k].join)
+                                (void)hipEventDestroy(s->spill_side[k].join);
                 }
                 if (s->ev0)
                         (void)hipEventDestroy(s->ev0);
@@ -1372,6 +1380,11 @@ static int spill_setup(vrt_scene *s, int64_t rays, int64_t pixels, hipStream_t s
         }
         if (!s->spill_ev[k])
                 HIPCHK(hipEventCreateWithFlags(&s->spill_ev[k], hipEventDisableTiming));
+        if (!s->spill_side[k].st) {
+                HIPCHK(hipEventCreateWithFlags(&s->spill_side[k].fork, hipEventDisableTiming));
+                HIPCHK(hipEventCreateWithFlags(&s->spill_side[k].join, hipEventDisableTiming));
+                HIPCHK(hipStreamCreateWithFlags(&s->spill_side[k].st, hipStreamNonBlocking));
+        }
         if (!s->h_spill) {
                 HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&s->h_spill), 16 * sizeof(uint32_t),
                                      hipHostMallocDefault));
@@ -1469,7 +1482,8 @@ static int secondary_launch(vrt_scene *s, const RenderParams &p, int spp, int ra
         int waves = 0, units[8];
         s->spill_last = sq.nchunks > 0 ? set : -1;
         const hipError_t e = launch_secondary(p, spp, rank, nranks, scene_res(s), d_prim, d_vis, s_hit, s_tri,
-                                              s_vox, slot >= 0 ? &q : nullptr, st, &waves, units, &sq);
+                                              s_vox, slot >= 0 ? &q : nullptr, st, &waves, units, &sq,
+                                              set >= 0 && s->spill_side[set].st ? &s->spill_side[set] : nullptr);
         if (set >= 0)
                 if (int rc = spill_done(s, set, sq, st))
                         return rc;

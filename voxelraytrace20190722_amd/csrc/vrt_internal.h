@@ -528,13 +528,20 @@ hipError_t launch_pack_c(int nx, int ny, int rank, int nranks, int comps, const 
                          hipStream_t st);
 hipError_t launch_unpack_c(int nx, int ny, int nranks, int tiles_per_rank, int comps, const float *src, float *dst,
                            hipStream_t st);
+// A side stream of a compaction set and its fork / join events: the
+// deferred pixels' exact walk (k_secondary_defer) runs there beside the
+// streaming resume instead of after it on the launch's stream.
+struct SideLaunch {
+        hipStream_t st;
+        hipEvent_t fork, join;
+};
 // q: the launch's work queue (persistent kernel) or nullptr (one wave per
-// pixel)
+// pixel); side: nullptr = every kernel on st
 hipError_t launch_secondary(const RenderParams &rp, int spp, int rank,
                             int nranks, float res, float *prim, float *vis,
                             int32_t *s_hit, int32_t *s_tri, uint32_t *s_vox,
                             const WorkQueue *q, hipStream_t st, int *q_waves, int slice_units[8],
-                            const SpillQueues *sq = nullptr);
+                            const SpillQueues *sq = nullptr, const SideLaunch *side = nullptr);
 // the compaction settings of this build (VRT_SEC_SPILL*), cap left 0
 SpillQueues spill_defaults();
 // a path-selecting compile-time switch of the kernel build by name (false:

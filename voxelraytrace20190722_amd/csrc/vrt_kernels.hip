@@ -2220,11 +2220,15 @@ __global__ __launch_bounds__(kBlock) void k_primary1(RenderParams p, float *__re
 {
         __shared__ uint2 stk[kStack * kBlock];
         const int tid = threadIdx.x;
-        const int W8 = 8 * p.ntx, H8 = 8 * p.nty;
-        const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
-        if (i >= (int64_t)W8 * H8)
+        const int W8 = 8 * p.ntx;
+        // a wave per 8x8 tile (lane = 8 * row + column; tiles in raster
+        // order): 64 neighbouring rays walk much the same nodes, where a
+        // 64-pixel row strip spreads them 8x wider
+        const int64_t t = (int64_t)blockIdx.x * (kBlock / 64) + (tid >> 6);
+        if (t >= (int64_t)p.ntx * p.nty)
                 return;
-        const int px = (int)(i % W8), py = (int)(i / W8);
+        const int px = (int)(t % p.ntx) * 8 + (tid & 7), py = (int)(t / p.ntx) * 8 + ((tid >> 3) & 7);
+        const int64_t i = (int64_t)py * W8 + px;
         const CamParams &c = p.cam;
         const f3 dn = camera_dir(c.s, c.u, c.nf, c.e, c.z, c.nx, c.ny, px, py, 0.5f, 0.5f);
         const RayK r = make_rayk(mk3(c.origin[0], c.origin[1], c.origin[2]), dn, c.tmin, c.tmax);
@@ -2900,7 +2904,7 @@ SpillQueues spill_defaults()
 hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nranks, float res,
                             float *prim, float *vis, int32_t *s_hit, int32_t *s_tri,
                             uint32_t *s_vox, const WorkQueue *q, hipStream_t st, int *q_waves, int slice_units[8],
-                            const SpillQueues *sq)
+                            const SpillQueues *sq, const SideLaunch *side)
 {
         *q_waves = 0;
         for (int x = 0; x < 8; ++x)
@@ -2963,6 +2967,27 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                         slice_units[x] = slice_size((int)waves, x, VRT_SEC_SLICE_CHUNK);
                 if (hipError_t e = hipGetLastError())
                         return e;
+                // the deferred pixels (normally a few, each one long exact
+                // walk): a quarter of the resident grid, each wave gone after
+                // one load if none.  With a side stream they run beside the
+                // resume round (they write other pixels than its rays do: a
+                // deferred pixel stopped none), joined before the launch ends.
+                SecondaryParams dp = sp;
+                dp.sq.t_first = 0;
+                const dim3 dgrid((unsigned)std::max(8, (g / 4) & ~7));
+                auto defer_kern = w ? k_secondary_defer<true> : k_secondary_defer<false>;
+                const bool fork = fo && side && side->st;
+                if (fork) {
+                        if (hipError_t e = hipEventRecord(side->fork, st))
+                                return e;
+                        if (hipError_t e = hipStreamWaitEvent(side->st, side->fork, 0))
+                                return e;
+                        hipLaunchKernelGGL(defer_kern, dgrid, dim3(kSecPBlock), 0, side->st, dp);
+                        if (hipError_t e = hipGetLastError())
+                                return e;
+                        if (hipError_t e = hipEventRecord(side->join, side->st))
+                                return e;
+                }
                 if (spill) {
                         // the resume round: one resident generation walking
                         // queue 0's records to their ends (an empty queue ends
@@ -2988,13 +3013,11 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                         hipLaunchKernelGGL(w ? k_sec_resume<true> : k_sec_resume<false>, dim3(8), dim3(kSecPBlock), 0,
                                            st, rp2);
                 }
-                if (fo) {
-                        // the deferred pixels (normally a few): a quarter of the
-                        // resident grid, each wave gone after one load if none
-                        SecondaryParams dp = sp;
-                        dp.sq.t_first = 0;
-                        hipLaunchKernelGGL(w ? k_secondary_defer<true> : k_secondary_defer<false>,
-                                           dim3((unsigned)std::max(8, (g / 4) & ~7)), dim3(kSecPBlock), 0, st, dp);
+                if (fork) {
+                        if (hipError_t e = hipStreamWaitEvent(st, side->join, 0))
+                                return e;
+                } else if (fo) {
+                        hipLaunchKernelGGL(defer_kern, dgrid, dim3(kSecPBlock), 0, st, dp);
                 }
                 return hipGetLastError();
         }
