@@ -205,7 +205,7 @@ def test_frames_in_flight_match_oracle(proxy):
         tree.set_frames_in_flight(1)
 
 
-@pytest.mark.parametrize("flags", [0, vrt.TEST_SPILL_ALL])
+@pytest.mark.parametrize("flags", [0, vrt.TEST_SPILL_ALL, vrt.TEST_SEC_DEFER])
 def test_c5_frames_in_flight_match_oracle(proxy, flags):
     """bench.py's config-5 schedule: frames of 3 poses issued on 3 streams
     without a host sync (one primary-record / visibility buffer pair per
@@ -213,7 +213,10 @@ def test_c5_frames_in_flight_match_oracle(proxy, flags):
     scratch sized anew) -- every visibility image equals the oracle's.
     flags=TEST_SPILL_ALL: nearly every ray is saved and resumed (the
     compaction is the default build's path: vrt_build_flag), through the
-    scene's alternating scratch sets."""
+    scene's alternating scratch sets.  flags=TEST_SEC_DEFER: every odd pixel
+    goes to the exact walk, which runs on each scratch set's side stream
+    beside the streaming resume (forked from and joined back into the
+    frame's stream) while the other streams' frames run."""
     import torch
     tree, osc = scenes(proxy, 8)
     mn, mx = tree.root_box
