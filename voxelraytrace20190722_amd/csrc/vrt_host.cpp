@@ -1381,9 +1381,20 @@ static int spill_setup(vrt_scene *s, int64_t rays, int64_t pixels, hipStream_t s
         if (!s->spill_ev[k])
                 HIPCHK(hipEventCreateWithFlags(&s->spill_ev[k], hipEventDisableTiming));
         if (!s->spill_side[k].st) {
-                HIPCHK(hipEventCreateWithFlags(&s->spill_side[k].fork, hipEventDisableTiming));
-                HIPCHK(hipEventCreateWithFlags(&s->spill_side[k].join, hipEventDisableTiming));
-                HIPCHK(hipStreamCreateWithFlags(&s->spill_side[k].st, hipStreamNonBlocking));
+                // all three or none (a set without a side stream runs the
+                // deferred walk on the launch's stream)
+                SideLaunch sl{};
+                if (hipEventCreateWithFlags(&sl.fork, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&sl.join, hipEventDisableTiming) == hipSuccess &&
+                    hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking) == hipSuccess) {
+                        s->spill_side[k] = sl;
+                } else {
+                        (void)hipGetLastError();
+                        if (sl.fork)
+                                (void)hipEventDestroy(sl.fork);
+                        if (sl.join)
+                                (void)hipEventDestroy(sl.join);
+                }
         }
         if (!s->h_spill) {
                 HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&s->h_spill), 16 * sizeof(uint32_t),
