@@ -2213,6 +2213,32 @@ __device__ __forceinline__ uint64_t pcg_advance(uint64_t s, uint64_t n)
         return am * s + ap;
 }
 
+// pcg_advance(s, 3 * lane) for the 64 lanes as (multiplier, increment)
+// pairs, made at compile time by the same loop: a pixel's lane-staggered
+// start state is one 16-B load and a 64-bit multiply-add instead of a
+// divergent 8-step jump with four 64-bit products per step.
+struct PcgJump3 {
+        uint64_t ac[64][2];
+        constexpr PcgJump3() : ac()
+        {
+                for (int l = 0; l < 64; ++l) {
+                        uint64_t n = 3u * (uint64_t)l, am = 1, ap = 0, cm = kPcgMul, cp = kPcgInc;
+                        while (n) {
+                                if (n & 1) {
+                                        am *= cm;
+                                        ap = ap * cm + cp;
+                                }
+                                cp = (cm + 1) * cp;
+                                cm *= cm;
+                                n >>= 1;
+                        }
+                        ac[l][0] = am;
+                        ac[l][1] = ap;
+                }
+        }
+};
+__constant__ PcgJump3 c_pcg_jump3 = PcgJump3();
+
 // Pass 1: pixel-centre primary ray (Camera::gen_rays1, VRT/camera.cc:77-93)
 // over the 8*(n/8) render area, one pixel per lane -> {hit, hit xyz, normal}.
 template <bool kR64>
@@ -2318,7 +2344,8 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         const f3 hp = mk3(pr[1], pr[2], pr[3]);
         const f3 nrm = mk3(pr[4], pr[5], pr[6]);
         const uint64_t seed = 0xc01dbeefULL ^ (uint64_t)((uint64_t)py * (uint64_t)p.nx + (uint64_t)px);
-        uint64_t st = pcg_advance(seed, 3 * (uint64_t)lane);
+        const ulonglong2 jl = reinterpret_cast<const ulonglong2 *>(c_pcg_jump3.ac)[lane];
+        uint64_t st = jl.x * seed + jl.y;  // pcg_advance(seed, 3 * lane)
         int have = 0;
         while (have < p.spp) {  // wave-uniform
                 uint64_t s2 = st;
