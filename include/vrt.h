@@ -466,7 +466,7 @@ const char *vrt_build_id(void);
 /* The value of one path-selecting compile-time switch of this build (e.g.
  * "VRT_SEC_SPILL_T": config 5's compaction threshold, 0 = no compaction;
  * "VRT_SEC_SLICE_CHUNK", "VRT_SLICE_CHUNK": the persistent kernels' slice
- * chunks; "VRT_DEAL_BLOCK" / "VRT_DEAL_WEIGHT" / "VRT_DEAL_SPAN": the tile
+ * chunks; "VRT_SEC_TAKE": config-5 pixels per dequeue; "VRT_DEAL_BLOCK" / "VRT_DEAL_WEIGHT" / "VRT_DEAL_SPAN": the tile
  * deal; "VRT_LIGHT_BUDGET" / "VRT_PRIM_BUDGET": the trace walks' budgets);
  * VRT_E_INVALID for a name the build does not know.  Lets a test assert which
  * path a build takes. */

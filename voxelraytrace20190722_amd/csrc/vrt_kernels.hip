@@ -2302,6 +2302,12 @@ struct SecondaryParams {
 
 // the persistent config-5 kernels (k_secondary_p, k_sec_resume): 4-wave workgroups
 constexpr int kSecPBlock = 256;
+// pixels a k_secondary_p wave takes per dequeue (one device-scope atomic)
+#ifndef VRT_SEC_TAKE
+#define VRT_SEC_TAKE 2
+#endif
+constexpr uint32_t kSecTake = VRT_SEC_TAKE;
+static_assert(kSecTake >= 1, "VRT_SEC_TAKE");
 #ifndef VRT_SECP_WAVES_PER_EU
 #define VRT_SECP_WAVES_PER_EU 6
 #endif
@@ -2323,11 +2329,21 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         // render_unit): its divisions are redone, not held in SGPRs
         int ntx = p.W8 >> 3, nty = p.H8 >> 3, nr = p.nranks, rk = p.rank;
         asm volatile("" : "+s"(ntx), "+s"(nty), "+s"(nr), "+s"(rk));
-        const TileDeal dl = tile_deal(ntx, nty, nr);
-        if ((k >> 6) >= (int64_t)deal_count(dl, rk))
-                return;
         int tx, ty;
-        deal_tile(dl, rk, (int)(k >> 6), tx, ty);
+        if (nr == 1) {
+                // one rank: raster order (deal_tile's own one-rank form),
+                // without tile_deal / deal_count's divisions
+                if ((k >> 6) >= (int64_t)ntx * nty)
+                        return;
+                const int T = (int)(k >> 6);
+                tx = T % ntx;
+                ty = T / ntx;
+        } else {
+                const TileDeal dl = tile_deal(ntx, nty, nr);
+                if ((k >> 6) >= (int64_t)deal_count(dl, rk))
+                        return;
+                deal_tile(dl, rk, (int)(k >> 6), tx, ty);
+        }
         const int px = tx * 8 + (int)(k & 7), py = ty * 8 + (int)((k >> 3) & 7);
         const int64_t pix = (int64_t)py * p.W8 + px;
         const float *pr = p.prim + 8 * pix;
@@ -2871,12 +2887,16 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
                 if (n <= 0)
                         continue;
                 for (;;) {
-                        const uint32_t u = take_unit(p.q.ctr + x * kQueueStride) - p.q.base[x];
+                        // kSecTake consecutive pixels per dequeue (every add is
+                        // kSecTake: launch_secondary's base accounting)
+                        const uint32_t u = take_n(p.q.ctr + x * kQueueStride, kSecTake) - p.q.base[x];
                         if (u >= (uint32_t)n)
                                 break;
-                        secondary_pixel<kR64, kAny, kSecPBlock, kFastOnly>(
-                                p, (int64_t)slice_unit(p.units, x, (int)u, VRT_SEC_SLICE_CHUNK), lane, stk + tid,
-                                pts[wave], cur);
+                        const uint32_t e = min(u + kSecTake, (uint32_t)n);
+                        for (uint32_t v = u; v < e; ++v)
+                                secondary_pixel<kR64, kAny, kSecPBlock, kFastOnly>(
+                                        p, (int64_t)slice_unit(p.units, x, (int)v, VRT_SEC_SLICE_CHUNK), lane,
+                                        stk + tid, pts[wave], cur);
                 }
         }
         if (kAny)
@@ -2989,9 +3009,14 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                                 sp.sq.t_first = 64;
                 }
                 hipLaunchKernelGGL(kern, dim3(g), dim3(kSecPBlock), 0, st, sp);
-                *q_waves = g * (kSecPBlock / 64);
-                for (int x = 0; x < 8; ++x)
-                        slice_units[x] = slice_size((int)waves, x, VRT_SEC_SLICE_CHUNK);
+                // every add is kSecTake: the successful takes cover a slice's
+                // pixels rounded up to whole takes, and each wave's one failing
+                // take per slice adds kSecTake too (queue_release)
+                *q_waves = g * (kSecPBlock / 64) * (int)kSecTake;
+                for (int x = 0; x < 8; ++x) {
+                        const int n = slice_size((int)waves, x, VRT_SEC_SLICE_CHUNK);
+                        slice_units[x] = (n + (int)kSecTake - 1) / (int)kSecTake * (int)kSecTake;
+                }
                 if (hipError_t e = hipGetLastError())
                         return e;
                 // the deferred pixels (normally a few, each one long exact
@@ -4581,6 +4606,7 @@ bool build_flag(const char *name, int64_t *value)
                 { "VRT_SEC_SPILL_T", VRT_SEC_SPILL_T },
 
                 { "VRT_SEC_SLICE_CHUNK", VRT_SEC_SLICE_CHUNK },
+                { "VRT_SEC_TAKE", VRT_SEC_TAKE },
 
                 { "VRT_SLICE_CHUNK", VRT_SLICE_CHUNK },
                 { "VRT_DEAL_BLOCK", VRT_DEAL_BLOCK },
