@@ -378,6 +378,15 @@ struct vrt_scene {
         hipStream_t spill_stream[2] = {};  // the set's last user (a stream keeps its set)
         // per set: the side stream of its deferred-pixel walk, fork / join
         SideLaunch spill_side[2] = {};
+        // multi-rank tile deals tabled on the device (RenderParams::tile_xy),
+        // one per (tiles, ranks, rank) used, built on first use by a kernel
+        // on that call's stream (ev), kept until the scene is destroyed
+        struct DealMap {
+                int ntx, nty, nranks, rank;
+                uint32_t *d;
+                hipEvent_t ev;
+        };
+        std::vector<DealMap> dmaps;
         uint32_t *h_spill = nullptr;       // pinned: per set, its last launch's round counters (ctr[0..7])
         uint32_t spill_want = 0;           // queue-0 chunks the next launch sizes for (0: first estimate)
         int spill_next = 0;
@@ -1058,6 +1067,11 @@ extern "C" void vrt_scene_destroy(vrt_scene *s)
                         if (s->spill_side[k].join)
                                 (void)hipEventDestroy(s->spill_side[k].join);
                 }
+                for (auto &m : s->dmaps) {
+                        (void)hipEventSynchronize(m.ev);
+                        (void)hipEventDestroy(m.ev);
+                        (void)hipFree(m.d);
+                }
                 if (s->ev0)
                         (void)hipEventDestroy(s->ev0);
                 if (s->ev1)
@@ -1578,6 +1592,45 @@ static int ensure_lm(vrt_scene *s, int i)
         return VRT_OK;
 }
 
+// The rank's tabled deal (RenderParams::tile_xy) for nranks > 1, built on
+// first use on stream st; a stream other than the builder's waits for the
+// build.  nullptr (the kernels then compute the deal): one rank, tile grids
+// of 2^16 or more, more than kDealMaps deals in use, or no memory.
+constexpr size_t kDealMaps = 32;
+static const uint32_t *deal_map(vrt_scene *s, int ntx, int nty, int nranks, int rank, hipStream_t st)
+{
+        if (nranks <= 1 || ntx >= 65536 || nty >= 65536)
+                return nullptr;
+        for (auto &m : s->dmaps)
+                if (m.ntx == ntx && m.nty == nty && m.nranks == nranks && m.rank == rank) {
+                        if (hipEventQuery(m.ev) != hipSuccess && hipStreamWaitEvent(st, m.ev, 0) != hipSuccess) {
+                                (void)hipGetLastError();
+                                return nullptr;
+                        }
+                        return m.d;
+                }
+        const int n = deal_count(tile_deal(ntx, nty, nranks), rank);
+        if (n <= 0 || s->dmaps.size() >= kDealMaps)
+                return nullptr;
+        vrt_scene::DealMap m{ ntx, nty, nranks, rank, nullptr, nullptr };
+        if (hipMalloc(reinterpret_cast<void **>(&m.d), (size_t)n * sizeof(uint32_t)) != hipSuccess) {
+                (void)hipGetLastError();
+                return nullptr;
+        }
+        if (hipEventCreateWithFlags(&m.ev, hipEventDisableTiming) != hipSuccess ||
+            launch_deal_map(ntx, nty, nranks, rank, m.d, st) != hipSuccess || hipEventRecord(m.ev, st) != hipSuccess) {
+                (void)hipGetLastError();
+                // a launch that got as far as the stream finishes before the free
+                (void)hipStreamSynchronize(st);
+                if (m.ev)
+                        (void)hipEventDestroy(m.ev);
+                (void)hipFree(m.d);
+                return nullptr;
+        }
+        s->dmaps.push_back(m);
+        return m.d;
+}
+
 extern "C" int vrt_render_tiles_device(vrt_scene *s, const vrt_camera *cam,
                                        const vrt_film *film, int rank,
                                        int nranks, int image_layout,
@@ -1600,6 +1653,7 @@ extern "C" int vrt_render_tiles_device(vrt_scene *s, const vrt_camera *cam,
         p.image_layout = image_layout;
         p.out = d_out;
         hipStream_t st = static_cast<hipStream_t>(stream);
+        p.tile_xy = deal_map(s, p.ntx, p.nty, nranks, rank, st);
         HIPCHK(hipEventRecord(s->ev0, st));
         if (int rc = render_launch(s, p, false, st))
                 return rc;
@@ -1930,6 +1984,8 @@ extern "C" int vrt_render_secondary_device(vrt_scene *s, const vrt_camera *cam,
         RenderParams p;
         fill_render_params(s, cam, film, 0, 1, &p);
         hipStream_t st = static_cast<hipStream_t>(stream);
+        // the secondary rays' share (the primary pass covers every pixel)
+        p.tile_xy = deal_map(s, p.ntx, p.nty, nranks, rank, st);
         HIPCHK(hipEventRecord(s->ev0, st));
         if (int rc = secondary_launch(s, p, spp, rank, nranks, d_prim, d_vis, nullptr, nullptr, nullptr, st))
                 return rc;

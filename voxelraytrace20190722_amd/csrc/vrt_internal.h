@@ -410,6 +410,10 @@ struct RenderParams {
         float *out;
         SampleOut so;
         WorkQueue q;           // persistent launches only
+        // nranks > 1: this rank's tiles in deal order, tx | ty << 16 each
+        // (k_deal_map, cached per scene), read with a scalar load instead of
+        // tile_deal / deal_tile's divisions per unit; nullptr: computed
+        const uint32_t *tile_xy;
 };
 
 // ---- full trace() -------------------------------------
@@ -548,6 +552,9 @@ SpillQueues spill_defaults();
 // unknown name) -- vrt_build_flag
 bool build_flag(const char *name, int64_t *value);
 hipError_t launch_light(const LightParams &p, hipStream_t st);
+// out[k] = rank's k-th tile of the deal (deal_tile), tx | ty << 16, for k <
+// deal_count (ntx, nty < 2^16)
+hipError_t launch_deal_map(int ntx, int nty, int nranks, int rank, uint32_t *out, hipStream_t st);
 hipError_t light_diag_copy(void *host, size_t bytes);  // VRT_LIGHT_DIAG builds
 // samp: n x 6 floats followed by room for their sorted copy (n x 6);
 // seg_start: max_seg entries (>= non-empty leaves), nseg zeroed (by

@@ -1802,7 +1802,16 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                 int ntx = p.ntx, nty = p.nty, nr = p.nranks, rk = p.rank;
                 if (!kSamples)
                         asm volatile("" : "+s"(ntx), "+s"(nty), "+s"(nr), "+s"(rk));
-                deal_tile(tile_deal(ntx, nty, nr), rk, k, tx, ty);
+                if (p.tile_xy) {
+                        // the rank's deal, tabled (constant address space,
+                        // wave-uniform k: a scalar load)
+                        typedef const __attribute__((address_space(4))) uint32_t ConstU;
+                        const uint32_t v = ((ConstU *)p.tile_xy)[k];
+                        tx = (int)(v & 0xFFFFu);
+                        ty = (int)(v >> 16);
+                } else {
+                        deal_tile(tile_deal(ntx, nty, nr), rk, k, tx, ty);
+                }
                 // the tile is wave-uniform: keep it in SGPRs (the deal's
                 // divisions may run on the VALU), not in VGPRs held -- and
                 // spilled -- across the march
@@ -2287,6 +2296,7 @@ __global__ __launch_bounds__(kBlock) void k_primary1(RenderParams p, float *__re
 // gets exactly the reference's s-th accepted point.
 struct SecondaryParams {
         DevScene sc;
+        const uint32_t *tile_xy;  // nranks > 1: the rank's tiles (RenderParams::tile_xy) or nullptr
         int32_t nx, W8, H8, spp;
         int32_t rank, nranks;  // this rank's 8x8 tiles: tile_deal
         float res;
@@ -2338,6 +2348,14 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
                 const int T = (int)(k >> 6);
                 tx = T % ntx;
                 ty = T / ntx;
+        } else if (p.tile_xy) {
+                // the rank's deal, tabled (p.units = its tiles x 64)
+                if (k >= (int64_t)p.units)
+                        return;
+                typedef const __attribute__((address_space(4))) uint32_t ConstU;
+                const uint32_t v = ((ConstU *)p.tile_xy)[k >> 6];
+                tx = (int)(v & 0xFFFFu);
+                ty = (int)(v >> 16);
         } else {
                 const TileDeal dl = tile_deal(ntx, nty, nr);
                 if ((k >> 6) >= (int64_t)deal_count(dl, rk))
@@ -2939,6 +2957,29 @@ __global__ __launch_bounds__(kSecPBlock, VRT_SECP_WAVES_PER_EU) void k_secondary
 #endif
 static_assert(kSpillStack >= kStack, "SpillRec stack");
 
+// The rank's tiles in deal order (RenderParams::tile_xy): one thread per
+// tile, deal_tile itself.
+__global__ __launch_bounds__(256) void k_deal_map(int ntx, int nty, int nranks, int rank, int n,
+                                                  uint32_t *__restrict__ out)
+{
+        const int k = (int)(blockIdx.x * 256 + threadIdx.x);
+        if (k >= n)
+                return;
+        int tx, ty;
+        deal_tile(tile_deal(ntx, nty, nranks), rank, k, tx, ty);
+        out[k] = (uint32_t)tx | (uint32_t)ty << 16;
+}
+
+hipError_t launch_deal_map(int ntx, int nty, int nranks, int rank, uint32_t *out, hipStream_t st)
+{
+        const int n = deal_count(tile_deal(ntx, nty, nranks), rank);
+        if (n <= 0)
+                return hipSuccess;
+        hipLaunchKernelGGL(k_deal_map, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ntx, nty, nranks, rank, n,
+                           out);
+        return hipGetLastError();
+}
+
 SpillQueues spill_defaults()
 {
         SpillQueues q;
@@ -2979,6 +3020,7 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
         sp.s_tri = s_tri;
         sp.s_vox = s_vox;
         sp.test_flags = rp.test_flags;
+        sp.tile_xy = nranks > 1 ? rp.tile_xy : nullptr;
         // pixels of this rank: its 8x8 tiles (tile_deal)
         const int64_t mine = deal_count(tile_deal(rp.ntx, rp.nty, nranks), rank);
         const int64_t waves = mine * 64;
