@@ -1269,6 +1269,10 @@ static void fill_render_params(vrt_scene *s, const vrt_camera *cam,
         p->rank = rank;
         p->nranks = nranks;
         p->tiles_this_rank = deal_count(tile_deal(p->ntx, p->nty, nranks), rank);
+        // k * ceil(2^40 / ntx) >> 40 == k / ntx for k < 2^40 / ntx, which
+        // k < 2^24 and ntx < 2^16 guarantee
+        if (p->ntx > 0 && p->ntx < (1 << 16) && (int64_t)p->ntx * p->nty < ((int64_t)1 << 24))
+                p->ntx_magic = (((uint64_t)1 << 40) + (uint64_t)p->ntx - 1) / (uint64_t)p->ntx;
         p->test_flags = g_test_flags.load();
 }
 

@@ -414,6 +414,9 @@ struct RenderParams {
         // (k_deal_map, cached per scene), read with a scalar load instead of
         // tile_deal / deal_tile's divisions per unit; nullptr: computed
         const uint32_t *tile_xy;
+        // one rank: ceil(2^40 / ntx), so a tile index k < 2^24 splits into
+        // (k % ntx, k / ntx) with one multiply (rank_tile); 0: divide
+        uint64_t ntx_magic;
 };
 
 // ---- full trace() -------------------------------------

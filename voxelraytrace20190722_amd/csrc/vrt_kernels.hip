@@ -1767,6 +1767,28 @@ __device__ __forceinline__ f3 shade_hit(const DevScene &sc, const RayK &r,
 // Primary render: an 8x8 tile = 4 waves of 4x4 pixels x 4 samples, one wave
 // per workgroup (a finished wave frees its slot and LDS at once).
 // ---------------------------------------------------------------------------
+// This rank's k-th tile (wave-uniform k): one rank with a magic divisor ->
+// one multiply (RenderParams::ntx_magic: the raster order deal_tile gives one
+// rank); several ranks with a tabled deal -> one scalar load (tile_xy);
+// otherwise deal_tile itself.
+__device__ __forceinline__ void rank_tile(int ntx, int nty, int nr, int rk, uint64_t magic, const uint32_t *tab,
+                                          int k, int &tx, int &ty)
+{
+        if (nr == 1 && magic) {
+                const uint32_t q = (uint32_t)(((uint64_t)(uint32_t)k * magic) >> 40);
+                ty = (int)q;
+                tx = k - (int)q * ntx;
+        } else if (tab) {
+                // constant address space, wave-uniform index: a scalar load
+                typedef const __attribute__((address_space(4))) uint32_t ConstU;
+                const uint32_t v = ((ConstU *)tab)[k];
+                tx = (int)(v & 0xFFFFu);
+                ty = (int)(v >> 16);
+        } else {
+                deal_tile(tile_deal(ntx, nty, nr), rk, k, tx, ty);
+        }
+}
+
 constexpr int kRenderBlock = 64;
 // One work unit of the primary render: the 4x4-pixel quadrant `wave` of
 // this rank's k-th 8x8 tile, 4 gen_rays4 samples per pixel, one ray per
@@ -1802,16 +1824,7 @@ __device__ __forceinline__ bool render_unit(const RenderParams &p, int k, int wa
                 int ntx = p.ntx, nty = p.nty, nr = p.nranks, rk = p.rank;
                 if (!kSamples)
                         asm volatile("" : "+s"(ntx), "+s"(nty), "+s"(nr), "+s"(rk));
-                if (p.tile_xy) {
-                        // the rank's deal, tabled (constant address space,
-                        // wave-uniform k: a scalar load)
-                        typedef const __attribute__((address_space(4))) uint32_t ConstU;
-                        const uint32_t v = ((ConstU *)p.tile_xy)[k];
-                        tx = (int)(v & 0xFFFFu);
-                        ty = (int)(v >> 16);
-                } else {
-                        deal_tile(tile_deal(ntx, nty, nr), rk, k, tx, ty);
-                }
+                rank_tile(ntx, nty, nr, rk, p.ntx_magic, p.tile_xy, k, tx, ty);
                 // the tile is wave-uniform: keep it in SGPRs (the deal's
                 // divisions may run on the VALU), not in VGPRs held -- and
                 // spilled -- across the march
@@ -2342,7 +2355,8 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
         int tx, ty;
         if (nr == 1) {
                 // one rank: raster order (deal_tile's own one-rank form),
-                // without tile_deal / deal_count's divisions
+                // without tile_deal / deal_count's divisions (the magic
+                // divisor of rank_tile costs this kernel 20 B/lane of scratch)
                 if ((k >> 6) >= (int64_t)ntx * nty)
                         return;
                 const int T = (int)(k >> 6);
@@ -2352,10 +2366,7 @@ __device__ __forceinline__ void secondary_pixel(const SecondaryParams &p, int64_
                 // the rank's deal, tabled (p.units = its tiles x 64)
                 if (k >= (int64_t)p.units)
                         return;
-                typedef const __attribute__((address_space(4))) uint32_t ConstU;
-                const uint32_t v = ((ConstU *)p.tile_xy)[k >> 6];
-                tx = (int)(v & 0xFFFFu);
-                ty = (int)(v >> 16);
+                rank_tile(ntx, nty, nr, rk, 0, p.tile_xy, (int)(k >> 6), tx, ty);
         } else {
                 const TileDeal dl = tile_deal(ntx, nty, nr);
                 if ((k >> 6) >= (int64_t)deal_count(dl, rk))
@@ -3712,7 +3723,7 @@ __device__ __forceinline__ bool tile_lane_at(const RenderParams &p, int u, int t
                 return false;
         k = u / kQ;
         int tx, ty;
-        deal_tile(tile_deal(p.ntx, p.nty, p.nranks), p.rank, k, tx, ty);
+        rank_tile(p.ntx, p.nty, p.nranks, p.rank, p.ntx_magic, p.tile_xy, k, tx, ty);
         const int wave = (u % kQ) + (tid >> 6), lane = tid & 63;
         s = lane & 3;
         const int pix = lane >> 2;
@@ -4496,7 +4507,7 @@ __global__ __launch_bounds__(64, VRT_CONES_WAVES_PER_EU) void k_cones_film(Trace
         const int lane = threadIdx.x;
         const int k = u / kQ, wave = u % kQ;
         int tx, ty;
-        deal_tile(tile_deal(p.r.ntx, p.r.nty, p.r.nranks), p.r.rank, k, tx, ty);
+        rank_tile(p.r.ntx, p.r.nty, p.r.nranks, p.r.rank, p.r.ntx_magic, p.r.tile_xy, k, tx, ty);
         const int s = lane & 3, pix = lane >> 2;
         const int lx = (wave & 1) * 4 + (pix & 3), ly = (wave >> 1) * 4 + (pix >> 2);
         const int px = tx * 8 + lx, py = ty * 8 + ly;
