@@ -470,3 +470,23 @@ def test_roofline_names_the_busier_issue_pipe():
         assert r["bound"] == want
         assert r["frac"] == pytest.approx(max(vf, sf), abs=1e-4)
         assert r["salu"]["instr_per_launch"] == round(salu)
+
+
+def test_magic_tile_divisor_is_exact():
+    """rank_tile's one-rank split (vrt_kernels.hip) divides a tile index k <
+    2^24 by ntx < 2^16 as (k * ceil(2^40 / ntx)) >> 40 (fill_render_params
+    sets the magic only in that range): exact at every k next to a multiple
+    of ntx, for every ntx up to 4096 and a sample above, up to k = 2^24 - 1."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    for ntx in list(range(1, 4097)) + [int(x) for x in rng.integers(4097, 1 << 16, 300)] + [(1 << 16) - 1]:
+        m = ((1 << 40) + ntx - 1) // ntx
+        lim = min((1 << 24) - 1, (1 << 24) // ntx * ntx + ntx - 1)
+        q = np.unique(np.concatenate([np.arange(0, 64), np.linspace(0, lim // ntx, 200).astype(np.int64),
+                                      [lim // ntx - 1, lim // ntx]]))
+        q = q[q >= 0]
+        k = np.concatenate([q * ntx, q * ntx - 1, q * ntx + ntx - 1])
+        k = k[(k >= 0) & (k < (1 << 24))].astype(object)
+        got = [(int(x) * m) >> 40 for x in k]
+        want = [int(x) // ntx for x in k]
+        assert got == want, ntx
