@@ -317,7 +317,8 @@ int vrt_secondary_spill_stats(vrt_scene *s, int64_t stats[7]);
  * (vrt_scene_info().device_bytes): per-call scratch kept between calls --
  * config 5's compaction queues (*spill_bytes, may be NULL), the light-map
  * build's scratch and light-map sets, the trace records, the host-output
- * image. */
+ * image, the tabled tile deals of multi-rank calls (4 B per tile of the
+ * rank). */
 int vrt_scene_scratch_bytes(vrt_scene *s, int64_t *bytes, int64_t *spill_bytes);
 
 /* The kernels' own travorder sort (std::sort of the 8 Items by dist,

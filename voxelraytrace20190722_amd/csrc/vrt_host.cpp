@@ -2013,6 +2013,8 @@ extern "C" int vrt_scene_scratch_bytes(vrt_scene *s, int64_t *bytes, int64_t *sp
                         t += (int64_t)lm_set_bytes(s->nodes.size());
                 t += (int64_t)ts.rec_bytes;
         }
+        for (const auto &m : s->dmaps)  // the tabled multi-rank deals
+                t += (int64_t)deal_count(tile_deal(m.ntx, m.nty, m.nranks), m.rank) * (int64_t)sizeof(uint32_t);
         *bytes = t;
         if (spill_bytes)
                 *spill_bytes = sp;
