@@ -3090,8 +3090,13 @@ hipError_t launch_secondary(const RenderParams &rp, int spp, int rank, int nrank
                         hipLaunchKernelGGL(defer_kern, dgrid, dim3(kSecPBlock), 0, side->st, dp);
                         if (hipError_t e = hipGetLastError())
                                 return e;
-                        if (hipError_t e = hipEventRecord(side->join, side->st))
+                        if (hipError_t e = hipEventRecord(side->join, side->st)) {
+                                // no join for the caller's stream to wait on: the
+                                // deferred walk finishes before the set can be
+                                // reused or freed (its event covers st only)
+                                (void)hipStreamSynchronize(side->st);
                                 return e;
+                        }
                 }
                 if (spill) {
                         // the resume round: one resident generation walking
