@@ -1631,7 +1631,14 @@ static const uint32_t *deal_map(vrt_scene *s, int ntx, int nty, int nranks, int 
                 (void)hipFree(m.d);
                 return nullptr;
         }
-        s->dmaps.push_back(m);
+        try {
+                s->dmaps.push_back(m);
+        } catch (const std::bad_alloc &) {
+                (void)hipEventSynchronize(m.ev);
+                (void)hipEventDestroy(m.ev);
+                (void)hipFree(m.d);
+                return nullptr;
+        }
         return m.d;
 }
 
